@@ -1,0 +1,223 @@
+/*
+ * vpcsum.h -- C-ABI of libvpcsum.so, the MI355X (gfx950) batched Internet
+ * checksum engine for vproxy's vswitch.
+ *
+ * The library replaces the per-packet Java checksum path
+ *   io.vproxy.base.util.Utils.calculateChecksum / calculateChecksumIntermediate /
+ *   calculateChecksumDoFinal          (base/src/main/java/io/vproxy/base/util/Utils.java:778-801)
+ *   Utils.buildPseudoIPv4Header / buildPseudoIPv6Header          (Utils.java:758-776)
+ *   Ipv4Packet.__updateChecksum                                   (vpacket/Ipv4Packet.java:209-217)
+ *   TcpPacket.updateChecksumWithIPv4 / IPv6                       (vpacket/TcpPacket.java:475-485, 508-518)
+ *   UdpPacket.updateChecksumWithIPv4 / IPv6                       (vpacket/UdpPacket.java:136-164)
+ *   IcmpPacket.__updateChecksum / updateChecksumWithIPv6          (vpacket/IcmpPacket.java:64-74, 124-135)
+ * with ONE batched GPU launch per flush point (Iface.completeTx, Switch.java:1076-1078), in the
+ * same flag-and-flush shape the XDP path already uses for its native checksum
+ * (SwitchUtils.checksumFlagsFor, core/.../vswitch/util/SwitchUtils.java:297-316;
+ *  XDPIface.sendPacket / completeTx, core/.../vswitch/iface/XDPIface.java:100-178, 227-243).
+ *
+ * Two entry-point families:
+ *   1. vpcsum_*                      plain C, return 0 on success, <0 on error
+ *                                    (message via vpcsum_last_error()).
+ *   2. Java_io_vproxy_vpcsum_VPCsum_* PNI convention (base/src/main/c-generated/pni.h:15-82):
+ *                                    int f(PNIEnv_<ret>* env, args...), 0 = ok, -1 = exception
+ *                                    stored in env->ex, result in env->return_.
+ *
+ * No torch types, no CUDA types: plain pointers and sizes.  Device pointers are
+ * hipMalloc'd (or torch) device memory; `stream` is a hipStream_t passed as void*.
+ */
+#ifndef VPCSUM_H
+#define VPCSUM_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VPCSUM_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------ */
+/* Data formats                                                             */
+/* ------------------------------------------------------------------------ */
+
+/* Per-packet descriptor flags (which sums are dirty).
+ * F_IP / F_L4 are the batched form of AbstractPacket.isRequireUpdatingChecksum()
+ * on the IP packet and on its upper-layer packet (AbstractPacket.java:38-65,
+ * Ipv4Packet.java:219-234, Ipv6Packet.java:219-236), i.e. XDP's VP_CSUM_IP / VP_CSUM_UP. */
+#define VPCSUM_F_IP    0x01u /* IPv4 header checksum (field L3+10)                        */
+#define VPCSUM_F_L4    0x02u /* TCP(+16) / UDP(+6) / ICMP(+2) / ICMPv6(+2) checksum        */
+#define VPCSUM_F_RAW   0x04u /* Utils.calculateChecksum(buf, len) over [l3_off, l3_off+l3_len);
+                                result in out bits 0..15; nothing else is interpreted       */
+
+typedef struct vpcsum_desc {
+    uint64_t l3_off;   /* byte offset of the L3 (IP) header inside the arena               */
+    uint16_t l3_len;   /* IPv4 totalLength / IPv6 40+payloadLength (L2 padding excluded,
+                          Ipv4Packet.java:100-103, Ipv6Packet.java:103-106)                  */
+    uint16_t l4_off;   /* L4 header offset relative to l3_off (ihl*4, or 40+ext headers)    */
+    uint8_t  l3_ver;   /* 4 or 6                                                             */
+    uint8_t  l4_proto; /* 6 TCP, 17 UDP, 1 ICMP, 58 ICMPv6; anything else: no L4 sum          */
+    uint8_t  flags;    /* VPCSUM_F_*                                                          */
+    uint8_t  rsv;      /* must be 0                                                          */
+} vpcsum_desc_t;       /* 16 bytes, naturally aligned                                        */
+
+/* Output word per packet: bits 0..15 = IPv4 header checksum, bits 16..31 = L4 checksum
+ * (host-order values, exactly the ints Java writes with ByteArray.int16). */
+
+/* Status byte per packet (optional output). */
+#define VPCSUM_S_IP_OK       0x01u /* verify: stored IPv4 header checksum == recomputed   */
+#define VPCSUM_S_L4_OK       0x02u /* verify: stored L4 checksum == recomputed            */
+#define VPCSUM_S_UDP_NOCSUM  0x04u /* UDP with stored checksum 0 (RFC 768 "no checksum")  */
+#define VPCSUM_S_DONE        0x40u /* descriptor processed                                */
+#define VPCSUM_S_BAD_DESC    0x80u /* descriptor rejected (bounds/lengths); nothing written */
+
+/* Batch modes. */
+#define VPCSUM_MODE_COMPUTE  0x00u /* compute dirty sums                                    */
+#define VPCSUM_MODE_VERIFY   0x01u /* compute and compare with the stored fields (ingress)  */
+#define VPCSUM_MODE_WRITE    0x10u /* also write results big-endian into the arena in place */
+
+/* NAT rewrite entry for IPv4 packets (SwitchUtils.applyNat, SwitchUtils.java:522-542;
+ * Ipv4Packet.setSrc/setDst :433-458, TcpPacket/UdpPacket.setSrcPort/setDstPort,
+ * Ipv4Packet.setTtl :401-407 via IPInputRoute.java:79-91). All multi-byte values in
+ * NETWORK byte order, exactly the bytes written into the packet. 16 bytes. */
+#define VPCSUM_NAT_SRC      0x01u
+#define VPCSUM_NAT_DST      0x02u
+#define VPCSUM_NAT_SPORT    0x04u
+#define VPCSUM_NAT_DPORT    0x08u
+#define VPCSUM_NAT_DEC_TTL  0x10u
+typedef struct vpcsum_nat4 {
+    uint8_t  src[4];
+    uint8_t  dst[4];
+    uint8_t  sport[2];
+    uint8_t  dport[2];
+    uint8_t  mask;     /* VPCSUM_NAT_*  */
+    uint8_t  rsv[3];
+} vpcsum_nat4_t;
+
+/* NAT modes. */
+#define VPCSUM_NAT_RFC1624     0x00u /* incremental update (RFC 1624 eqn. 3); header bytes only */
+#define VPCSUM_NAT_STRICT_JAVA 0x01u /* rewrite, then full recompute: identical to Java for ANY
+                                        input, including invalid input checksums              */
+
+/* ------------------------------------------------------------------------ */
+/* Library / device                                                         */
+/* ------------------------------------------------------------------------ */
+int         vpcsum_abi_version(void);
+const char* vpcsum_last_error(void);          /* thread-local message of the last failure */
+int         vpcsum_device_count(int* out_n);
+int         vpcsum_set_device(int device);
+
+/* ------------------------------------------------------------------------ */
+/* Device-resident batch ops (async on `stream`; all pointers device memory) */
+/* ------------------------------------------------------------------------ */
+
+/* Compute / verify the checksums named by each descriptor's flags.
+ * d_out (n words) and d_status (n bytes) may each be NULL. */
+int vpcsum_compute_async(const uint8_t* d_arena, uint64_t arena_len,
+                         const vpcsum_desc_t* d_desc, uint32_t n,
+                         uint32_t* d_out, uint8_t* d_status,
+                         uint32_t mode, void* stream);
+
+/* NAT / TTL rewrite + checksum update, in place in the arena. */
+int vpcsum_nat4_async(uint8_t* d_arena, uint64_t arena_len,
+                      const vpcsum_desc_t* d_desc, const vpcsum_nat4_t* d_rw, uint32_t n,
+                      uint8_t* d_status, uint32_t nat_mode, void* stream);
+
+/* Build descriptors on the GPU by parsing Ethernet frames (EthernetPacket.from,
+ * Ipv4Packet.from, Ipv6Packet.from rules). frame i = [d_frame_off[i], +d_frame_len[i]).
+ * flags = VPCSUM_F_* applied to every IP packet found; non-IP / unparsable frames get
+ * flags 0 and status VPCSUM_S_BAD_DESC. */
+int vpcsum_parse_ether_async(const uint8_t* d_arena, uint64_t arena_len,
+                             const uint64_t* d_frame_off, const uint32_t* d_frame_len, uint32_t n,
+                             uint8_t flags, vpcsum_desc_t* d_desc, uint8_t* d_status, void* stream);
+
+/* Streaming-read ceiling probe: reads `bytes` from d_buf with 16-B lanes, writes one word per
+ * block into d_sink.  Used by bench.py to report a measured HBM read roof next to 8 TB/s. */
+int vpcsum_read_probe_async(const uint8_t* d_buf, uint64_t bytes, uint32_t* d_sink,
+                            uint32_t grid, void* stream);
+
+/* Synthetic workload generator (bench / tests): deterministic counter-based splitmix64 bytes,
+ * identical to oracle/csum_oracle.c:orc_synth_frame.  workload: see VPCSUM_SYNTH_*. */
+#define VPCSUM_SYNTH_C1_UDP64     1  /* IPv4/UDP L3 50 B                     */
+#define VPCSUM_SYNTH_C2_TCP1500   2  /* IPv4/TCP L3 1500 B                   */
+#define VPCSUM_SYNTH_C3_MIXED     3  /* IPv4 {64,576,1500} x {UDP,TCP,ICMP}  */
+#define VPCSUM_SYNTH_C4_V6JUMBO   4  /* IPv6/TCP L3 9000 B                   */
+#define VPCSUM_SYNTH_FUZZ         5  /* v4/v6, options, odd lengths, all protos */
+int vpcsum_synth_async(uint8_t* d_arena, uint64_t arena_len, uint32_t n, uint32_t stride,
+                       uint32_t l3_pad, uint32_t workload, uint64_t seed, uint64_t first_index,
+                       vpcsum_desc_t* d_desc, void* stream);
+
+/* Kernel timing on the caller's stream (HIP events). */
+int vpcsum_event_create(void** ev);
+int vpcsum_event_destroy(void* ev);
+int vpcsum_event_record(void* ev, void* stream);
+int vpcsum_event_elapsed_ms(void* start, void* end, float* ms);
+int vpcsum_stream_sync(void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Host-memory API (what the Java side drives): host arena + descriptors,   */
+/* library-owned device buffers, pinned staging, async submit / wait.        */
+/* ------------------------------------------------------------------------ */
+typedef struct vpcsum_ctx vpcsum_ctx_t;
+
+int vpcsum_ctx_create(int device, uint64_t max_arena_bytes, uint32_t max_pkts, vpcsum_ctx_t** out);
+int vpcsum_ctx_destroy(vpcsum_ctx_t* ctx);
+/* Page-lock a long-lived host arena (e.g. an AF_XDP umem, UMem.java:36-44) once, so that
+ * submits from it DMA directly without a staging copy. */
+int vpcsum_ctx_register_arena(vpcsum_ctx_t* ctx, void* h_arena, uint64_t len);
+int vpcsum_ctx_unregister_arena(vpcsum_ctx_t* ctx, void* h_arena);
+/* Copy the frames the descriptors touch to the device, run the batch, copy results back
+ * (and, with VPCSUM_MODE_WRITE, the checksum fields back into the host frames).
+ * Returns a ticket; results are valid after vpcsum_ctx_wait(ticket). */
+int vpcsum_ctx_submit(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena_len,
+                      const vpcsum_desc_t* h_desc, uint32_t n,
+                      uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket);
+int vpcsum_ctx_wait(vpcsum_ctx_t* ctx, uint64_t ticket);
+/* Pipelined host->device->host throughput helper: processes a host arena of n fixed-stride
+ * frames in `chunks` double-buffered pieces over two streams (H2D || kernel || D2H). */
+int vpcsum_ctx_pipeline(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint32_t stride, uint32_t copy_bytes,
+                        const vpcsum_desc_t* h_desc, uint32_t n, uint32_t* h_out,
+                        uint32_t mode, uint32_t chunks);
+
+/* ------------------------------------------------------------------------ */
+/* PNI entry points (bound by io.vproxy.vpcsum.VPCsum)   */
+/* Layout copied from the PNI convention, base/src/main/c-generated/pni.h   */
+/* ------------------------------------------------------------------------ */
+typedef struct PNIException_vpcsum {
+    char*   type;
+    char    message[4096];
+    int32_t errno_;
+} PNIException_vpcsum;
+
+typedef struct PNIEnv_vpcsum_long {
+    PNIException_vpcsum ex;
+    union { int64_t return_; struct { uint64_t a, b; } placeholder_; };
+} PNIEnv_vpcsum_long;
+
+typedef struct PNIEnv_vpcsum_int {
+    PNIException_vpcsum ex;
+    union { int32_t return_; struct { uint64_t a, b; } placeholder_; };
+} PNIEnv_vpcsum_int;
+
+typedef struct PNIEnv_vpcsum_void {
+    PNIException_vpcsum ex;
+    struct { uint64_t a, b; } placeholder_;
+} PNIEnv_vpcsum_void;
+
+/* VPCsum.create(int device, long maxArena, int maxPkts) -> long ctx */
+int Java_io_vproxy_vpcsum_VPCsum_create(PNIEnv_vpcsum_long* env, int32_t device, int64_t maxArena, int32_t maxPkts);
+/* VPCsum.registerArena(long ctx, MemorySegment arena, long len) */
+int Java_io_vproxy_vpcsum_VPCsum_registerArena(PNIEnv_vpcsum_void* env, int64_t ctx, void* arena, int64_t len);
+/* VPCsum.submit(long ctx, MemorySegment arena, long arenaLen, MemorySegment desc, int n,
+ *               MemorySegment out, MemorySegment status, int mode) -> long ticket */
+int Java_io_vproxy_vpcsum_VPCsum_submit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                        void* desc, int32_t n, void* out, void* status, int32_t mode);
+/* VPCsum.waitFor(long ctx, long ticket) */
+int Java_io_vproxy_vpcsum_VPCsum_waitFor(PNIEnv_vpcsum_void* env, int64_t ctx, int64_t ticket);
+/* VPCsum.close(long ctx) */
+int Java_io_vproxy_vpcsum_VPCsum_close(PNIEnv_vpcsum_void* env, int64_t ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VPCSUM_H */
