@@ -1,0 +1,365 @@
+"""GPU parity: libvpcsum.so (HIP, gfx950) vs the CPU oracle, bit-exact, through the C-ABI.
+
+Small cases compare every output word/status/byte with the oracle; the full-size C2 batch
+(1M x 1500 B) is checked through size-independent properties (compute+write -> verify all OK,
+idempotence) plus a random sample of packets against the oracle.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pcaputil import l3_offset, read_pcap
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def V():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vproxy_amd import vpcsum
+    vpcsum.lib()
+    return vpcsum
+
+
+def dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def gpu_compute(V, arena_np, desc_np, mode=O.MODE_COMPUTE, team_log2=0, write=False):
+    import torch
+    arena = dev(arena_np.copy())
+    d = V.desc_to_tensor(desc_np)
+    n = len(desc_np)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    V.compute(arena, d, n, out, st, mode | (O.MODE_WRITE if write else 0), team_log2)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32), st.cpu().numpy(), arena.cpu().numpy()
+
+
+def kat_batch():
+    kats = json.load(open(os.path.join(GOLD, "kat.json")))["kats"]
+    frames, infos = [], []
+    for k in kats:
+        fr = bytes.fromhex(k["hex"])
+        info = O.parse_ether(fr)[0] if k["layer"] == "ether" else O.parse_l3(fr, 0, len(fr))[0]
+        frames.append(fr)
+        infos.append([info])
+        if "inner_l3_off" in k:
+            infos[-1].append(O.parse_l3(fr, k["inner_l3_off"], len(fr) - k["inner_l3_off"])[0])
+    return kats, frames, infos
+
+
+def pack(frames, infos, stride=None, pad=0):
+    stride = stride or (max(len(f) for f in frames) + 64 + pad)
+    arena = np.zeros(stride * len(frames), np.uint8)
+    rows = []
+    for i, (fr, inf) in enumerate(zip(frames, infos)):
+        base = i * stride + pad
+        arena[base:base + len(fr)] = np.frombuffer(fr, np.uint8)
+        for x in inf:
+            rows.append((base + x.l3_off, x.l3_len, x.l4_off, x.ver, x.proto, O.desc_flags_for(x), 0))
+    desc = np.array(rows, dtype=O.DESC_DTYPE)
+    return arena, desc
+
+
+@pytest.mark.parametrize("pad", [0, 1, 2, 3, 14, 15, 398])
+@pytest.mark.parametrize("team", [0, 2, 3, 5, 6])
+def test_kats_on_gpu(V, orc, pad, team):
+    kats, frames, infos = kat_batch()
+    arena, desc = pack(frames, infos, pad=pad)
+    out, st, _ = gpu_compute(V, arena, desc, O.MODE_VERIFY, team)
+    oout, ost = orc.process(arena, desc, O.MODE_VERIFY)
+    assert np.array_equal(out, oout)
+    assert np.array_equal(st, ost)
+    # pinned values from TestPacket.java
+    j = 0
+    for k, inf in zip(kats, infos):
+        pin = k["pinned"]
+        if "ip" in pin:
+            assert out[j] & 0xFFFF == pin["ip"]
+        if "l4" in pin:
+            assert out[j] >> 16 == pin["l4"]
+        if "inner_ip" in pin:
+            assert out[j + 1] & 0xFFFF == pin["inner_ip"] and out[j + 1] >> 16 == pin["inner_l4"]
+        j += len(inf)
+    assert np.all(st & O.S_DONE)
+
+
+def test_pcap_verify_on_gpu(V, orc):
+    frames, infos = [], []
+    for fn in sorted(os.listdir(os.path.join(GOLD, "pcap"))):
+        lt, pkts = read_pcap(os.path.join(GOLD, "pcap", fn))
+        for p in pkts:
+            off = l3_offset(lt, p)
+            if off is None:
+                continue
+            info, err = O.parse_l3(p, off, len(p) - off)
+            assert err is None
+            frames.append(p)
+            infos.append([info])
+    arena, desc = pack(frames, infos)
+    out, st, _ = gpu_compute(V, arena, desc, O.MODE_VERIFY)
+    oout, ost = orc.process(arena, desc, O.MODE_VERIFY)
+    assert np.array_equal(out, oout) and np.array_equal(st, ost)
+    assert len(desc) == 31
+    assert int(np.sum(st & O.S_IP_OK > 0)) == 31
+    assert int(np.sum(st & O.S_L4_OK > 0)) == 19   # 12 CHECKSUM_PARTIAL host-TX frames fail
+
+
+@pytest.mark.parametrize("workload", [O.SYNTH_C1, O.SYNTH_C2, O.SYNTH_C3, O.SYNTH_C4, O.SYNTH_FUZZ])
+@pytest.mark.parametrize("pad", [0, 1, 14, 398])
+def test_synth_matches_oracle_and_checksums(V, orc, workload, pad):
+    import torch
+    n = 600 if workload in (O.SYNTH_C4, O.SYNTH_FUZZ) else 3000
+    maxlen = 9000 if workload in (O.SYNTH_C4, O.SYNTH_FUZZ) else 1500
+    stride = ((pad + maxlen + 63) // 64) * 64
+    arena_o, desc_o = orc.synth(n, stride, pad, workload, O.SEED, first_index=12345)
+    arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    V.synth(arena, n, stride, pad, workload, O.SEED, 12345, d)
+    torch.cuda.synchronize()
+    assert np.array_equal(arena.cpu().numpy(), arena_o), "GPU generator differs from oracle generator"
+    assert np.array_equal(V.tensor_to_desc(d), desc_o)
+    for team in (0, 2, 6):
+        out, st, written = gpu_compute(V, arena_o, desc_o, O.MODE_COMPUTE, team, write=True)
+        a2 = arena_o.copy()
+        oout, ost = orc.process(a2, desc_o, O.MODE_COMPUTE, write=True)
+        assert np.array_equal(out, oout)
+        assert np.array_equal(st, ost)
+        assert np.array_equal(written, a2)
+    # written frames verify clean
+    out2, st2, _ = gpu_compute(V, written, desc_o, O.MODE_VERIFY)
+    want = np.where(desc_o["flags"] & O.F_IP, O.S_IP_OK, 0) | O.S_L4_OK | O.S_DONE
+    assert np.array_equal(st2 & ~np.uint8(O.S_UDP_NOCSUM), want.astype(np.uint8))
+    assert np.array_equal(out2, out)
+
+
+def test_raw_ranges(V, orc):
+    rng = np.random.default_rng(5)
+    lens = [0, 1, 2, 3, 5, 15, 16, 17, 31, 33, 63, 64, 65, 1499, 1500, 1501, 4097, 9000, 65535]
+    arena = rng.integers(0, 256, 200000, dtype=np.uint8)
+    arena[100000:110000] = 0
+    arena[120000:130000] = 0xFF
+    rows = []
+    for L in lens:
+        for off in (0, 1, 7, 100000 + 3, 120000 + 1, int(rng.integers(0, 100000))):
+            if off + L <= len(arena):
+                rows.append((off, L, 0, 0, 0, O.F_RAW, 0))
+    desc = np.array(rows, dtype=O.DESC_DTYPE)
+    out, st, _ = gpu_compute(V, arena, desc)
+    for r, o in zip(rows, out):
+        assert o == O.csum(arena[r[0]:r[0] + r[1]].tobytes()), r
+
+
+def test_bad_descriptors(V, orc):
+    arena = np.zeros(4096, np.uint8)
+    arena[0] = 0x45
+    rows = [
+        (4000, 200, 20, 4, 6, 3, 0),     # beyond arena
+        (0, 19, 20, 4, 6, 3, 0),         # too short
+        (0, 100, 22, 4, 6, 3, 0),        # l4_off not multiple of 4
+        (0, 100, 20, 5, 6, 3, 0),        # bad version
+        (0, 100, 20, 4, 58, 2, 0),       # ICMPv6 in IPv4
+        (0, 100, 20, 6, 6, 1, 0),        # IP sum requested on IPv6
+        (0, 30, 20, 4, 6, 2, 0),         # TCP segment shorter than its checksum field
+        (2 ** 63, 100, 20, 4, 6, 3, 0),  # absurd offset
+    ]
+    desc = np.array(rows, dtype=O.DESC_DTYPE)
+    out, st, after = gpu_compute(V, arena, desc, write=True)
+    oout, ost = orc.process(arena.copy(), desc)
+    assert np.all(st == O.S_BAD_DESC) and np.all(ost == O.S_BAD_DESC)
+    assert np.all(out == 0)
+    assert np.array_equal(after, arena)
+
+
+def _nat_batch(orc, n, seed=3, corrupt=0.0, udp_zero=0.0):
+    arena, desc = orc.synth(n, 2048, 0, O.SYNTH_C3, O.SEED, 777)
+    orc.process(arena, desc, O.MODE_COMPUTE, write=True)       # valid input checksums
+    rng = np.random.default_rng(seed)
+    rw = np.zeros(n, O.NAT4_DTYPE)
+    rw["src"] = rng.integers(0, 256, (n, 4))
+    rw["dst"] = rng.integers(0, 256, (n, 4))
+    rw["sport"] = rng.integers(0, 256, (n, 2))
+    rw["dport"] = rng.integers(0, 256, (n, 2))
+    rw["mask"] = rng.integers(0, 32, n)
+    for i in range(n):
+        l3 = int(desc[i]["l3_off"])
+        if rng.random() < corrupt:
+            arena[l3 + 10] ^= 0x5A
+            f = l3 + 20 + {6: 16, 17: 6, 1: 2}[int(desc[i]["l4_proto"])]
+            arena[f + 1] ^= 0x33
+        if desc[i]["l4_proto"] == 17 and rng.random() < udp_zero:
+            arena[l3 + 26] = 0
+            arena[l3 + 27] = 0
+    return arena, desc, rw
+
+
+def _gpu_nat(V, arena_np, desc, rw, mode):
+    import torch
+    arena = dev(arena_np.copy())
+    st = torch.zeros(len(desc), dtype=torch.uint8, device="cuda")
+    V.nat4(arena, V.desc_to_tensor(desc), dev(rw.view(np.uint8)), len(desc), st, mode)
+    torch.cuda.synchronize()
+    return arena.cpu().numpy(), st.cpu().numpy()
+
+
+def test_nat_rfc1624_bit_exact_on_valid_input(V, orc):
+    arena, desc, rw = _nat_batch(orc, 4000, udp_zero=0.1)
+    want = arena.copy()
+    orc.nat4_java(want, desc, rw)
+    got, st = _gpu_nat(V, arena, desc, rw, V.NAT_RFC1624)
+    assert np.all(st == O.S_DONE)
+    assert np.array_equal(got, want)
+
+
+def test_nat_strict_java_on_invalid_input(V, orc):
+    arena, desc, rw = _nat_batch(orc, 3000, seed=9, corrupt=0.3, udp_zero=0.2)
+    want = arena.copy()
+    orc.nat4_java(want, desc, rw)
+    got, st = _gpu_nat(V, arena, desc, rw, V.NAT_STRICT_JAVA)
+    assert np.array_equal(got, want)
+    # RFC 1624 diverges exactly where the input was wrong -- documented behaviour
+    got_fast, _ = _gpu_nat(V, arena, desc, rw, V.NAT_RFC1624)
+    assert not np.array_equal(got_fast, want)
+
+
+def test_nat_golden(V):
+    d = json.load(open(os.path.join(GOLD, "nat.json")))
+    for mode in (0, 1):
+        for c in d["cases"]:
+            fr = bytes.fromhex(c["before"])
+            info, _ = O.parse_l3(fr, c["l3_off"], len(fr) - c["l3_off"])
+            desc = np.array([(info.l3_off, info.l3_len, info.l4_off, 4, info.proto, O.desc_flags_for(info), 0)],
+                            dtype=O.DESC_DTYPE)
+            rw = np.zeros(1, O.NAT4_DTYPE)
+            rw[0]["src"] = [1, 2, 3, 4]
+            rw[0]["dst"] = [1, 2, 3, 4]
+            rw[0]["sport"] = [0, 121]
+            rw[0]["dport"] = [0, 121]
+            rw[0]["mask"] = c["mask"]
+            got, _ = _gpu_nat(V, np.frombuffer(fr, np.uint8), desc, rw, mode)
+            assert got.tobytes().hex() == c["after"], (c["kat"], c["rewrite"], mode)
+
+
+def test_parse_ether_matches_reference_rules(V):
+    import torch
+    frames = []
+    for fn in sorted(os.listdir(os.path.join(GOLD, "pcap"))):
+        lt, pkts = read_pcap(os.path.join(GOLD, "pcap", fn))
+        if lt == 1:
+            frames += pkts
+    kats = json.load(open(os.path.join(GOLD, "kat.json")))["kats"]
+    frames += [bytes.fromhex(k["hex"]) for k in kats if k["layer"] == "ether"]
+    # VLAN-tagged, IPv6 with one ext header, truncated, non-IP, padded frames
+    base = bytes.fromhex(kats[2]["hex"])
+    frames.append(base[:12] + b"\x81\x00\x00\x05" + base[12:])
+    frames.append(base + b"\x00" * 6)                        # Ethernet padding
+    frames.append(base[:30])                                 # truncated
+    frames.append(base[:12] + b"\x08\x06" + base[14:])       # ARP type
+    v6 = bytes.fromhex(kats[1]["hex"])
+    ext = bytes([58, 6]) + bytes(12)                         # hop-by-hop, hdrExtLen 6 -> 14 B
+    v6x = bytearray(v6[:40] + ext + v6[40:])
+    v6x[6] = 0
+    pl = len(v6x) - 40
+    v6x[4:6] = pl.to_bytes(2, "big")
+    frames.append(bytes(12) + b"\x86\xdd" + bytes(v6x))
+    frames.append(bytes(12) + b"\x86\xdd" + v6)
+    offs, lens = [], []
+    arena = bytearray()
+    for f in frames:
+        offs.append(len(arena))
+        lens.append(len(f))
+        arena += f + bytes((-len(f)) % 64)
+    n = len(frames)
+    a = dev(np.frombuffer(bytes(arena), np.uint8))
+    d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    V.parse_ether(a, dev(np.array(offs, np.uint64)), dev(np.array(lens, np.uint32)), n, d, st)
+    torch.cuda.synchronize()
+    got = V.tensor_to_desc(d)
+    stn = st.cpu().numpy()
+    for i, f in enumerate(frames):
+        info, err = O.parse_ether(f)
+        if info is None:
+            assert stn[i] == O.S_BAD_DESC, (i, err)
+            continue
+        assert stn[i] == 0
+        g = got[i]
+        assert int(g["l3_off"]) == offs[i] + info.l3_off
+        assert (g["l3_len"], g["l4_off"], g["l3_ver"], g["l4_proto"]) == (info.l3_len, info.l4_off, info.ver, info.proto)
+        assert g["flags"] == O.desc_flags_for(info)
+
+
+def test_context_host_api(V, orc):
+    arena, desc = orc.synth(5000, 2048, 14, O.SYNTH_C3, O.SEED, 99)
+    want_out, want_st = orc.process(arena, desc, O.MODE_COMPUTE)
+    ctx = V.Context(0, max_arena=16 << 20, max_pkts=8192)
+    out, st = ctx.run(arena, desc)
+    assert np.array_equal(out, want_out) and np.array_equal(st, want_st)
+    # registered (page-locked) arena, in-place write, then verify through the same context
+    ctx.register(arena)
+    a2 = arena.copy()
+    orc.process(a2, desc, O.MODE_COMPUTE, write=True)
+    out = np.zeros(len(desc), np.uint32)
+    t = ctx.submit(arena, desc, out, None, O.MODE_WRITE)
+    ctx.wait(t)
+    assert np.array_equal(arena, a2)
+    out, st = ctx.run(arena, desc, O.MODE_VERIFY)
+    assert np.all(st & O.S_L4_OK)
+    ctx.unregister(arena)
+    # two batches in flight
+    ta = ctx.submit(arena, desc[:2000], oa := np.zeros(2000, np.uint32))
+    tb = ctx.submit(arena, desc[2000:], ob := np.zeros(3000, np.uint32))
+    ctx.wait(tb)
+    ctx.wait(ta)
+    assert np.array_equal(np.concatenate([oa, ob]), want_out)
+    ctx.close()
+
+
+def test_context_pipeline(V, orc):
+    n, stride = 20000, 2048
+    arena, desc = orc.synth(n, stride, 0, O.SYNTH_C2, O.SEED, 5)
+    want, _ = orc.process(arena, desc)
+    out = np.zeros(n, np.uint32)
+    ctx = V.Context(0, max_arena=8 << 20, max_pkts=4096)
+    ctx.register(arena)
+    ctx.register(desc)
+    ctx.register(out)
+    ctx.pipeline(arena, stride, 1504, desc, out, chunks=8)
+    assert np.array_equal(out, want)
+    ctx.close()
+
+
+def test_full_size_c2_properties(V, orc):
+    """BASELINE config C2 at full size: 1,048,576 x 1500 B, stride 2048."""
+    import torch
+    n, stride = 1 << 20, 2048
+    arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    V.synth(arena, n, stride, 0, O.SYNTH_C2, O.SEED, 0, d)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    V.compute(arena, d, n, out, st, O.MODE_WRITE)
+    out2 = torch.zeros_like(out)
+    V.compute(arena, d, n, out2, st, O.MODE_VERIFY)
+    torch.cuda.synchronize()
+    stn = st.cpu().numpy()
+    assert np.all(stn == (O.S_DONE | O.S_IP_OK | O.S_L4_OK))
+    assert torch.equal(out, out2)
+    # random sample against the oracle (regenerated on the CPU from the same counters)
+    rng = np.random.default_rng(11)
+    idx = np.sort(rng.choice(n, 3000, replace=False))
+    o = out.cpu().numpy().view(np.uint32)
+    for i in idx[:3000]:
+        a1, d1 = orc.synth(1, stride, 0, O.SYNTH_C2, O.SEED, int(i))
+        w, _ = orc.process(a1, d1)
+        assert o[i] == w[0]

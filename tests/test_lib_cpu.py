@@ -1,0 +1,71 @@
+"""CPU-side checks of the product library: it builds, loads, and exports exactly the C-ABI
+that include/vpcsum.h declares (no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "vpcsum.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(\w+)\s*\(", src, re.M)))
+
+
+@pytest.fixture(scope="module")
+def libpath():
+    from vproxy_amd import build
+    return build.build()
+
+
+def test_header_declares_expected_surface():
+    fns = header_functions()
+    assert len(fns) >= 25
+    assert "vpcsum_compute_async" in fns and "Java_io_vproxy_vpcsum_VPCsum_submit" in fns
+
+
+def test_binding_lists_every_header_symbol():
+    from vproxy_amd import vpcsum
+    assert sorted(vpcsum.EXPORTS) == header_functions()
+
+
+def test_so_exports_every_declared_symbol(libpath):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", libpath], text=True)
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, missing
+
+
+def test_so_loads_and_reports_abi(libpath):
+    L = ctypes.CDLL(libpath)
+    for f in header_functions():
+        assert hasattr(L, f)
+    L.vpcsum_abi_version.restype = ctypes.c_int
+    assert L.vpcsum_abi_version() == 1
+
+
+def test_code_object_is_gfx950(libpath):
+    # the embedded HIP fat binary names its only target
+    data = open(libpath, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    assert b"gfx942" not in data and b"gfx90a" not in data
+
+
+def test_fails_loudly_without_library(monkeypatch, tmp_path):
+    from vproxy_amd import vpcsum
+    monkeypatch.setattr(vpcsum, "_lib", None)
+    monkeypatch.setattr(vpcsum, "LIB", str(tmp_path / "missing.so"))
+    with pytest.raises(vpcsum.VpcsumUnavailable):
+        vpcsum.lib()
+
+
+def test_descriptor_layout_matches_header():
+    from vproxy_amd import vpcsum
+    from oracle import oracle as O
+    assert vpcsum.DESC_DTYPE == O.DESC_DTYPE and vpcsum.DESC_DTYPE.itemsize == 16
+    assert vpcsum.NAT4_DTYPE.itemsize == 16
+    assert [vpcsum.DESC_DTYPE.fields[k][1] for k in vpcsum.DESC_DTYPE.names] == [0, 8, 10, 12, 13, 14, 15]

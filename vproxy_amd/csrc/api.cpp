@@ -1,0 +1,487 @@
+// api.cpp -- the C-ABI of libvpcsum.so (declared in include/vpcsum.h).
+//
+// Device-resident entry points validate arguments and launch the kernels of kernels.hip on
+// the caller's stream.  The context API is what the Java side drives (io.vproxy.vpcsum.VPCsum,
+// java/io/vproxy/vpcsum/VPCsum.java): host arena + descriptors in, checksums out, with the
+// batch flushed once per Iface.completeTx (core/.../vswitch/iface/XDPIface.java:227-243).
+// Errors: plain functions return <0 and set a thread-local message; PNI functions store the
+// exception in env->ex exactly as the PNI runtime expects (base/src/main/c-generated/pni.h:74-82).
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+#include "vpcsum.h"
+
+namespace vpcsum {
+
+static thread_local std::string g_err;
+
+static int fail(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return -1;
+}
+
+static int hipfail(hipError_t e, const char* what) {
+    return fail("%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+#define VPC_CHECK(expr, what)                         \
+    do {                                              \
+        hipError_t e__ = (expr);                      \
+        if (e__ != hipSuccess) return hipfail(e__, what); \
+    } while (0)
+
+int num_cus(int device) {
+    static std::mutex mu;
+    static std::vector<int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    if (device < 0) device = 0;
+    if ((int)cache.size() <= device) cache.resize(device + 1, 0);
+    if (cache[device] == 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || v <= 0) v = 256;
+        cache[device] = v;
+    }
+    return cache[device];
+}
+
+// Per-slot staging of one in-flight batch of a context.
+struct Slot {
+    uint8_t* d_arena = nullptr;
+    vpcsum_desc_t* d_desc = nullptr;
+    uint32_t* d_out = nullptr;
+    uint8_t* d_status = nullptr;
+    vpcsum_desc_t* h_desc = nullptr;   // pinned staging
+    uint32_t* h_out = nullptr;         // pinned staging
+    uint8_t* h_status = nullptr;       // pinned staging
+    uint8_t* h_arena = nullptr;        // pinned staging for unregistered arenas
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    // the batch currently owned by this slot
+    uint64_t ticket = 0;
+    bool busy = false;
+    uint32_t n = 0;
+    uint32_t mode = 0;
+    uint8_t* user_arena = nullptr;
+    const vpcsum_desc_t* user_desc = nullptr;
+    uint32_t* user_out = nullptr;
+    uint8_t* user_status = nullptr;
+};
+
+}  // namespace vpcsum
+
+struct vpcsum_ctx {
+    int device = 0;
+    uint64_t max_arena = 0;
+    uint32_t max_pkts = 0;
+    vpcsum::Slot slots[2];
+    uint64_t next_ticket = 1;
+    std::vector<std::pair<uint8_t*, uint64_t>> registered;
+    std::mutex mu;
+};
+
+using namespace vpcsum;
+
+extern "C" {
+
+int vpcsum_abi_version(void) { return VPCSUM_ABI_VERSION; }
+
+const char* vpcsum_last_error(void) { return g_err.c_str(); }
+
+int vpcsum_device_count(int* out_n) {
+    if (!out_n) return fail("vpcsum_device_count: out_n is NULL");
+    int n = 0;
+    VPC_CHECK(hipGetDeviceCount(&n), "hipGetDeviceCount");
+    *out_n = n;
+    return 0;
+}
+
+int vpcsum_set_device(int device) {
+    VPC_CHECK(hipSetDevice(device), "hipSetDevice");
+    return 0;
+}
+
+static int team_from_mode(uint32_t mode) { return (int)((mode >> 8) & 0xf); }
+
+int vpcsum_compute_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, uint32_t n,
+                         uint32_t* d_out, uint8_t* d_status, uint32_t mode, void* stream) {
+    if (n == 0) return 0;
+    if (!d_arena || !d_desc) return fail("vpcsum_compute_async: NULL arena or descriptors");
+    if (mode & ~(0xfffu | VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_compute_async: bad mode 0x%x", mode);
+    uint8_t* w = (mode & VPCSUM_MODE_WRITE) ? const_cast<uint8_t*>(d_arena) : nullptr;
+    // bits 12..27 of the mode word are unused; bits 8..11 = log2(lanes per packet) tuning hint
+    VPC_CHECK(launch_csum(d_arena, arena_len, d_desc, n, d_out, d_status, nullptr, mode, w, team_from_mode(mode), 0,
+                          (hipStream_t)stream),
+              "vpcsum_compute_async launch");
+    return 0;
+}
+
+int vpcsum_nat4_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const vpcsum_nat4_t* d_rw,
+                      uint32_t n, uint8_t* d_status, uint32_t nat_mode, void* stream) {
+    if (n == 0) return 0;
+    if (!d_arena || !d_desc || !d_rw) return fail("vpcsum_nat4_async: NULL arena, descriptors or rewrite table");
+    if (nat_mode & ~VPCSUM_NAT_STRICT_JAVA) return fail("vpcsum_nat4_async: bad nat_mode 0x%x", nat_mode);
+    hipStream_t s = (hipStream_t)stream;
+    if (nat_mode & VPCSUM_NAT_STRICT_JAVA) {
+        if (!d_status) return fail("vpcsum_nat4_async: strict-java mode needs a status buffer");
+        // pass 1: rewrite fields, record which sums went dirty (Java's checksumSkipped())
+        VPC_CHECK(launch_nat4(d_arena, arena_len, d_desc, d_rw, n, nullptr, d_status, nat_mode, s), "nat4 launch");
+        // pass 2: full recompute of the dirty sums, written in place (getRawPacket(0))
+        VPC_CHECK(launch_csum(d_arena, arena_len, d_desc, n, nullptr, d_status, d_status, VPCSUM_MODE_WRITE, d_arena,
+                              0, 0, s),
+                  "nat4 recompute launch");
+        return 0;
+    }
+    VPC_CHECK(launch_nat4(d_arena, arena_len, d_desc, d_rw, n, d_status, nullptr, nat_mode, s), "nat4 launch");
+    return 0;
+}
+
+int vpcsum_parse_ether_async(const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_frame_off,
+                             const uint32_t* d_frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* d_desc,
+                             uint8_t* d_status, void* stream) {
+    if (n == 0) return 0;
+    if (!d_arena || !d_frame_off || !d_frame_len || !d_desc) return fail("vpcsum_parse_ether_async: NULL argument");
+    VPC_CHECK(launch_parse_ether(d_arena, arena_len, d_frame_off, d_frame_len, n, flags, d_desc, d_status,
+                                 (hipStream_t)stream),
+              "parse launch");
+    return 0;
+}
+
+int vpcsum_read_probe_async(const uint8_t* d_buf, uint64_t bytes, uint32_t* d_sink, uint32_t grid, void* stream) {
+    if (!d_buf || !d_sink) return fail("vpcsum_read_probe_async: NULL argument");
+    VPC_CHECK(launch_read_probe(d_buf, bytes, d_sink, grid, (hipStream_t)stream), "read probe launch");
+    return 0;
+}
+
+int vpcsum_synth_async(uint8_t* d_arena, uint64_t arena_len, uint32_t n, uint32_t stride, uint32_t l3_pad,
+                       uint32_t workload, uint64_t seed, uint64_t first_index, vpcsum_desc_t* d_desc, void* stream) {
+    if (n == 0) return 0;
+    if (!d_arena) return fail("vpcsum_synth_async: NULL arena");
+    if (workload < VPCSUM_SYNTH_C1_UDP64 || workload > VPCSUM_SYNTH_FUZZ) return fail("vpcsum_synth_async: bad workload %u", workload);
+    const uint32_t maxlen = (workload == VPCSUM_SYNTH_C4_V6JUMBO || workload == VPCSUM_SYNTH_FUZZ) ? 9000
+                            : (workload == VPCSUM_SYNTH_C1_UDP64) ? 50 : 1500;
+    if ((uint64_t)l3_pad + maxlen > stride) return fail("vpcsum_synth_async: stride %u < l3_pad %u + %u", stride, l3_pad, maxlen);
+    if ((uint64_t)n * stride > arena_len) return fail("vpcsum_synth_async: arena too small");
+    VPC_CHECK(launch_synth(d_arena, arena_len, n, stride, l3_pad, workload, seed, first_index, d_desc,
+                           (hipStream_t)stream),
+              "synth launch");
+    return 0;
+}
+
+int vpcsum_event_create(void** ev) {
+    if (!ev) return fail("vpcsum_event_create: NULL");
+    hipEvent_t e;
+    VPC_CHECK(hipEventCreate(&e), "hipEventCreate");
+    *ev = (void*)e;
+    return 0;
+}
+int vpcsum_event_destroy(void* ev) {
+    VPC_CHECK(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy");
+    return 0;
+}
+int vpcsum_event_record(void* ev, void* stream) {
+    VPC_CHECK(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream), "hipEventRecord");
+    return 0;
+}
+int vpcsum_event_elapsed_ms(void* start, void* end, float* ms) {
+    if (!ms) return fail("vpcsum_event_elapsed_ms: NULL");
+    VPC_CHECK(hipEventSynchronize((hipEvent_t)end), "hipEventSynchronize");
+    VPC_CHECK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end), "hipEventElapsedTime");
+    return 0;
+}
+int vpcsum_stream_sync(void* stream) {
+    VPC_CHECK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Context (host memory) API
+// ------------------------------------------------------------------------------------------
+static void slot_free(Slot& s) {
+    if (s.d_arena) (void)hipFree(s.d_arena);
+    if (s.d_desc) (void)hipFree(s.d_desc);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.d_status) (void)hipFree(s.d_status);
+    if (s.h_desc) (void)hipHostFree(s.h_desc);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.h_status) (void)hipHostFree(s.h_status);
+    if (s.h_arena) (void)hipHostFree(s.h_arena);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = Slot();
+}
+
+int vpcsum_ctx_create(int device, uint64_t max_arena_bytes, uint32_t max_pkts, vpcsum_ctx_t** out) {
+    if (!out) return fail("vpcsum_ctx_create: out is NULL");
+    if (max_arena_bytes == 0 || max_pkts == 0) return fail("vpcsum_ctx_create: zero capacity");
+    VPC_CHECK(hipSetDevice(device), "hipSetDevice");
+    vpcsum_ctx* c = new vpcsum_ctx();
+    c->device = device;
+    c->max_arena = max_arena_bytes;
+    c->max_pkts = max_pkts;
+    for (auto& s : c->slots) {
+        hipError_t e = hipSuccess;
+        if ((e = hipMalloc((void**)&s.d_arena, max_arena_bytes + 64)) != hipSuccess ||
+            (e = hipMalloc((void**)&s.d_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t))) != hipSuccess ||
+            (e = hipMalloc((void**)&s.d_out, (size_t)max_pkts * 4)) != hipSuccess ||
+            (e = hipMalloc((void**)&s.d_status, (size_t)max_pkts)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t), 0)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_out, (size_t)max_pkts * 4, 0)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_status, (size_t)max_pkts, 0)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_arena, max_arena_bytes + 64, 0)) != hipSuccess ||
+            (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
+            for (auto& t : c->slots) slot_free(t);
+            delete c;
+            return hipfail(e, "vpcsum_ctx_create allocation");
+        }
+    }
+    *out = c;
+    return 0;
+}
+
+int vpcsum_ctx_destroy(vpcsum_ctx_t* c) {
+    if (!c) return 0;
+    (void)hipSetDevice(c->device);
+    for (auto& s : c->slots) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        slot_free(s);
+    }
+    for (auto& r : c->registered) (void)hipHostUnregister(r.first);
+    delete c;
+    return 0;
+}
+
+int vpcsum_ctx_register_arena(vpcsum_ctx_t* c, void* h_arena, uint64_t len) {
+    if (!c || !h_arena || len == 0) return fail("vpcsum_ctx_register_arena: bad argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterDefault), "hipHostRegister");
+    c->registered.emplace_back((uint8_t*)h_arena, len);
+    return 0;
+}
+
+int vpcsum_ctx_unregister_arena(vpcsum_ctx_t* c, void* h_arena) {
+    if (!c || !h_arena) return fail("vpcsum_ctx_unregister_arena: bad argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    for (size_t i = 0; i < c->registered.size(); ++i) {
+        if (c->registered[i].first == (uint8_t*)h_arena) {
+            VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
+            c->registered.erase(c->registered.begin() + i);
+            return 0;
+        }
+    }
+    return fail("vpcsum_ctx_unregister_arena: arena not registered");
+}
+
+static bool is_registered(vpcsum_ctx* c, const uint8_t* p, uint64_t len) {
+    for (auto& r : c->registered)
+        if (p >= r.first && p + len <= r.first + r.second) return true;
+    return false;
+}
+
+static int slot_finish(vpcsum_ctx* c, Slot& s) {
+    if (!s.busy) return 0;
+    VPC_CHECK(hipEventSynchronize(s.done), "hipEventSynchronize");
+    if (s.user_out) memcpy(s.user_out, s.h_out, (size_t)s.n * 4);
+    if (s.user_status) memcpy(s.user_status, s.h_status, s.n);
+    if ((s.mode & VPCSUM_MODE_WRITE) && s.user_arena) {
+        // place the GPU results into the caller's frames (big endian, as ByteArray.int16)
+        for (uint32_t i = 0; i < s.n; ++i) {
+            const vpcsum_desc_t& d = s.user_desc[i];
+            if (s.h_status[i] & VPCSUM_S_BAD_DESC) continue;
+            uint8_t* l3 = s.user_arena + d.l3_off;
+            const uint32_t w = s.h_out[i];
+            if (d.flags & VPCSUM_F_IP) { l3[10] = (uint8_t)(w >> 8); l3[11] = (uint8_t)w; }
+            if (d.flags & VPCSUM_F_L4) {
+                const int fld = d.l4_proto == 6 ? 16 : d.l4_proto == 17 ? 6 : 2;
+                l3[d.l4_off + fld] = (uint8_t)(w >> 24);
+                l3[d.l4_off + fld + 1] = (uint8_t)(w >> 16);
+            }
+        }
+    }
+    s.busy = false;
+    return 0;
+}
+
+int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, uint32_t n,
+                      uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket) {
+    if (!c || !ticket) return fail("vpcsum_ctx_submit: NULL context or ticket");
+    if (n > c->max_pkts) return fail("vpcsum_ctx_submit: %u packets > capacity %u", n, c->max_pkts);
+    if (n && (!h_arena || !h_desc)) return fail("vpcsum_ctx_submit: NULL arena or descriptors");
+    if (mode & ~(VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_ctx_submit: bad mode 0x%x", mode);
+    std::lock_guard<std::mutex> lk(c->mu);
+    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    const uint64_t t = c->next_ticket++;
+    Slot& s = c->slots[t & 1];
+    if (s.busy && slot_finish(c, s) != 0) return -1;
+
+    // byte span the descriptors touch (16-B aligned so device alignment == host alignment)
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const vpcsum_desc_t& d = h_desc[i];
+        if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) continue;   // kernel flags it BAD
+        lo = std::min(lo, d.l3_off);
+        hi = std::max(hi, d.l3_off + d.l3_len);
+    }
+    if (lo == UINT64_MAX) { lo = 0; hi = 0; }
+    lo &= ~(uint64_t)15;
+    const uint64_t span = hi - lo;
+    if (span > c->max_arena) return fail("vpcsum_ctx_submit: batch spans %llu bytes > capacity %llu",
+                                         (unsigned long long)span, (unsigned long long)c->max_arena);
+    // descriptors rebased to the device copy of [lo, hi)
+    for (uint32_t i = 0; i < n; ++i) {
+        s.h_desc[i] = h_desc[i];
+        if (h_desc[i].l3_off >= lo) s.h_desc[i].l3_off = h_desc[i].l3_off - lo;
+        else s.h_desc[i].l3_off = UINT64_MAX;   // out of span -> BAD in the kernel
+    }
+    VPC_CHECK(hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)n * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice, s.stream),
+              "H2D descriptors");
+    if (span) {
+        const uint8_t* src = h_arena + lo;
+        if (!is_registered(c, src, span)) {
+            memcpy(s.h_arena, src, span);   // pageable -> pinned staging
+            src = s.h_arena;
+        }
+        VPC_CHECK(hipMemcpyAsync(s.d_arena, src, span, hipMemcpyHostToDevice, s.stream), "H2D arena");
+    }
+    VPC_CHECK(launch_csum(s.d_arena, span, s.d_desc, n, s.d_out, s.d_status, nullptr, mode & VPCSUM_MODE_VERIFY,
+                          nullptr, 0, 0, s.stream),
+              "checksum launch");
+    VPC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream), "D2H out");
+    VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
+    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+    s.busy = true;
+    s.ticket = t;
+    s.n = n;
+    s.mode = mode;
+    s.user_arena = h_arena;
+    s.user_desc = h_desc;
+    s.user_out = h_out;
+    s.user_status = h_status;
+    *ticket = t;
+    return 0;
+}
+
+int vpcsum_ctx_wait(vpcsum_ctx_t* c, uint64_t ticket) {
+    if (!c) return fail("vpcsum_ctx_wait: NULL context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    Slot& s = c->slots[ticket & 1];
+    if (!s.busy || s.ticket != ticket) {
+        if (ticket == 0 || ticket >= c->next_ticket) return fail("vpcsum_ctx_wait: unknown ticket %llu", (unsigned long long)ticket);
+        return 0;   // already completed
+    }
+    return slot_finish(c, s);
+}
+
+int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint32_t copy_bytes,
+                        const vpcsum_desc_t* h_desc, uint32_t n, uint32_t* h_out, uint32_t mode, uint32_t chunks) {
+    if (!c || !h_arena || !h_desc || !h_out) return fail("vpcsum_ctx_pipeline: NULL argument");
+    if (chunks == 0) chunks = 1;
+    if (copy_bytes > stride) return fail("vpcsum_ctx_pipeline: copy_bytes > stride");
+    if (mode & ~VPCSUM_MODE_VERIFY) return fail("vpcsum_ctx_pipeline: bad mode");
+    std::lock_guard<std::mutex> lk(c->mu);
+    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    for (auto& s : c->slots)
+        if (s.busy && slot_finish(c, s) != 0) return -1;
+    const uint32_t per = (n + chunks - 1) / chunks;
+    if (per > c->max_pkts || (uint64_t)per * stride > c->max_arena)
+        return fail("vpcsum_ctx_pipeline: chunk of %u frames exceeds context capacity", per);
+    const bool pinned = is_registered(c, h_arena, (uint64_t)n * stride);
+    if (!pinned) return fail("vpcsum_ctx_pipeline: host arena must be registered (vpcsum_ctx_register_arena)");
+    const bool desc_pinned = is_registered(c, (const uint8_t*)h_desc, (uint64_t)n * sizeof(vpcsum_desc_t));
+    const bool out_pinned = is_registered(c, (const uint8_t*)h_out, (uint64_t)n * 4);
+    if (!desc_pinned || !out_pinned) return fail("vpcsum_ctx_pipeline: descriptors and out must be registered");
+    for (uint32_t k = 0; k < chunks; ++k) {
+        const uint32_t i0 = k * per;
+        if (i0 >= n) break;
+        const uint32_t m = std::min(per, n - i0);
+        Slot& s = c->slots[k & 1];
+        // descriptors of this chunk address the device slot as frame (i - i0) * stride: the
+        // caller's descriptors are relative to frame i0 once i0 * stride is subtracted
+        VPC_CHECK(hipMemcpyAsync(s.d_desc, h_desc + i0, (size_t)m * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice,
+                                 s.stream),
+                  "pipeline H2D desc");
+        VPC_CHECK(hipMemcpy2DAsync(s.d_arena, stride, h_arena + (uint64_t)i0 * stride, stride, copy_bytes, m,
+                                   hipMemcpyHostToDevice, s.stream),
+                  "pipeline H2D frames");
+        VPC_CHECK(launch_csum(s.d_arena - (uint64_t)i0 * stride, (uint64_t)(i0 + m) * stride, s.d_desc, m, s.d_out,
+                              nullptr, nullptr, mode, nullptr, 0, 0, s.stream),
+                  "pipeline launch");
+        VPC_CHECK(hipMemcpyAsync(h_out + i0, s.d_out, (size_t)m * 4, hipMemcpyDeviceToHost, s.stream), "pipeline D2H");
+    }
+    for (auto& s : c->slots) VPC_CHECK(hipStreamSynchronize(s.stream), "pipeline sync");
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// PNI entry points
+// ------------------------------------------------------------------------------------------
+static int pni_throw(void* env, const char* type) {
+    PNIException_vpcsum* ex = (PNIException_vpcsum*)env;
+    ex->type = (char*)type;
+    strncpy(ex->message, g_err.c_str(), sizeof(ex->message));
+    ex->message[sizeof(ex->message) - 1] = '\0';
+    return -1;
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_create(PNIEnv_vpcsum_long* env, int32_t device, int64_t maxArena, int32_t maxPkts) {
+    if (maxArena <= 0 || maxPkts <= 0) {
+        fail("maxArena and maxPkts must be positive");
+        return pni_throw(env, "java.lang.IllegalArgumentException");
+    }
+    vpcsum_ctx_t* c = nullptr;
+    if (vpcsum_ctx_create(device, (uint64_t)maxArena, (uint32_t)maxPkts, &c) != 0) return pni_throw(env, "java.io.IOException");
+    env->return_ = (int64_t)(intptr_t)c;
+    return 0;
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_registerArena(PNIEnv_vpcsum_void* env, int64_t ctx, void* arena, int64_t len) {
+    if (len <= 0) {
+        fail("len must be positive");
+        return pni_throw(env, "java.lang.IllegalArgumentException");
+    }
+    if (vpcsum_ctx_register_arena((vpcsum_ctx_t*)(intptr_t)ctx, arena, (uint64_t)len) != 0)
+        return pni_throw(env, "java.io.IOException");
+    return 0;
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_submit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen, void* desc,
+                                        int32_t n, void* out, void* status, int32_t mode) {
+    if (n < 0 || arenaLen < 0) {
+        fail("negative length");
+        return pni_throw(env, "java.lang.IllegalArgumentException");
+    }
+    uint64_t t = 0;
+    if (vpcsum_ctx_submit((vpcsum_ctx_t*)(intptr_t)ctx, (uint8_t*)arena, (uint64_t)arenaLen, (const vpcsum_desc_t*)desc,
+                          (uint32_t)n, (uint32_t*)out, (uint8_t*)status, (uint32_t)mode, &t) != 0)
+        return pni_throw(env, "java.io.IOException");
+    env->return_ = (int64_t)t;
+    return 0;
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_waitFor(PNIEnv_vpcsum_void* env, int64_t ctx, int64_t ticket) {
+    if (vpcsum_ctx_wait((vpcsum_ctx_t*)(intptr_t)ctx, (uint64_t)ticket) != 0) return pni_throw(env, "java.io.IOException");
+    return 0;
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_close(PNIEnv_vpcsum_void* env, int64_t ctx) {
+    (void)env;
+    vpcsum_ctx_destroy((vpcsum_ctx_t*)(intptr_t)ctx);
+    return 0;
+}
+
+}  // extern "C"

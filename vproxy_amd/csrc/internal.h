@@ -1,0 +1,30 @@
+// Internal launch interface between the C-ABI layer (api.cpp) and the kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "vpcsum.h"
+
+namespace vpcsum {
+
+// Lanes per packet ("team") for the checksum kernel.  0 = auto.
+// mode bits 8..11 carry an explicit log2(team) (tuning / tests); see api.cpp.
+hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
+                       uint32_t* out, uint8_t* status, const uint8_t* flags_override, uint32_t mode,
+                       uint8_t* arena_w, int team_log2, int grid_override, hipStream_t stream);
+
+hipError_t launch_nat4(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const vpcsum_nat4_t* rw,
+                       uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream);
+
+hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const uint64_t* frame_off,
+                              const uint32_t* frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* desc,
+                              uint8_t* status, hipStream_t stream);
+
+hipError_t launch_read_probe(const uint8_t* buf, uint64_t bytes, uint32_t* sink, uint32_t grid, hipStream_t stream);
+
+hipError_t launch_synth(uint8_t* arena, uint64_t arena_len, uint32_t n, uint32_t stride, uint32_t l3_pad,
+                        uint32_t workload, uint64_t seed, uint64_t first_index, vpcsum_desc_t* desc,
+                        hipStream_t stream);
+
+int num_cus(int device);
+
+}  // namespace vpcsum

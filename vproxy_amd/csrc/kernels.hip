@@ -1,0 +1,674 @@
+// kernels.hip -- gfx950 (MI355X, CDNA4) kernels of libvpcsum.
+//
+// The hot path restates, batched, the Java checksum code of vproxy's vswitch:
+//   Utils.calculateChecksumIntermediate / DoFinal     base/src/main/java/io/vproxy/base/util/Utils.java:778-801
+//   Utils.buildPseudoIPv4Header / IPv6Header          Utils.java:758-776
+//   Ipv4Packet.__updateChecksum                       base/src/main/java/io/vproxy/vpacket/Ipv4Packet.java:209-217
+//   TcpPacket.updateChecksumWithIPv4/IPv6             vpacket/TcpPacket.java:475-485, 508-518
+//   UdpPacket.updateChecksumWithIPv4/IPv6 (0->ffff)   vpacket/UdpPacket.java:136-164
+//   IcmpPacket.__updateChecksum / WithIPv6            vpacket/IcmpPacket.java:64-74, 124-135
+//
+// Arithmetic: the Java loop folds the end-around carry after every big-endian 16-bit word.
+// Here each lane sums little-endian 32-bit words of 16-byte aligned chunks into 64 bits,
+// the team (lanes of one packet) reduces with wave shuffles, and the sum is folded once and
+// byte-swapped when the range starts at an even address.  That is bit-exact with the Java
+// per-step fold, including the 0x0000/0xffff representation (both give 0 only for an
+// all-zero input; tests/test_oracle_golden.py::test_deferred_fold_equivalence).
+//
+// No MFMA: this is a bandwidth-bound integer reduction (~0.4 integer ops per byte).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "vpcsum.h"
+#include "internal.h"
+
+namespace vpcsum {
+
+// ------------------------------------------------------------------------------------------
+// small helpers
+// ------------------------------------------------------------------------------------------
+
+// Bytes of the dword at relative byte position d that fall inside [lo, hi).
+__device__ __forceinline__ uint32_t bmask(int d, int lo, int hi) {
+    int s = min(max(lo - d, 0), 4);
+    int e = min(max(hi - d, 0), 4);
+    uint32_t me = e >= 4 ? 0xffffffffu : ((1u << (e << 3)) - 1u);
+    uint32_t ms = s >= 4 ? 0xffffffffu : ((1u << (s << 3)) - 1u);
+    return me & ~ms;
+}
+
+// End-around-carry fold of a 64-bit sum of LE words to 16 bits; 0 only for 0.
+__device__ __forceinline__ uint32_t fold64(uint64_t x) {
+    uint64_t t = (x & 0xffffffffull) + (x >> 32);
+    t = (t & 0xffff) + (t >> 16);
+    t = (t & 0xffff) + (t >> 16);
+    t = (t & 0xffff) + (t >> 16);
+    return (uint32_t)t;
+}
+__device__ __forceinline__ uint32_t fold32(uint32_t x) {
+    x = (x & 0xffff) + (x >> 16);
+    x = (x & 0xffff) + (x >> 16);
+    return x;
+}
+__device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xff) << 8) | (v >> 8); }
+// A sum taken over a byte range that starts at an even absolute address is byte-swapped
+// relative to the big-endian word grid of that range (RFC 1071 byte-order independence).
+__device__ __forceinline__ uint32_t orient(uint32_t v, int start) { return (start & 1) ? v : bswap16(v); }
+
+__device__ __forceinline__ int l4_field(int proto) {
+    return proto == 6 ? 16 : proto == 17 ? 6 : (proto == 1 || proto == 58) ? 2 : -1;
+}
+
+// Internal flag set by the NAT kernel on descriptors it rejected (strict-Java mode hands its
+// per-packet dirty flags to the checksum kernel through flags_override).
+constexpr int kFlagRejected = 0x80;
+
+template <int TEAM>
+__device__ __forceinline__ uint32_t team_sum(uint32_t v) {
+#pragma unroll
+    for (int m = TEAM / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, TEAM);
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// K1: compute / verify kernel.  One team of TEAM lanes per packet; each lane owns the
+// 16-byte chunks k = tl, tl+TEAM, ... of [align16(L3), L3+need).  U chunks per lane are
+// loaded (global_load_dwordx4) before any is consumed so every lane keeps U*16 bytes in
+// flight; chunks fully inside the L4 payload take the 8-instruction fast path, the few
+// header / tail chunks take the byte-masked path.
+// ------------------------------------------------------------------------------------------
+struct PktPlan {
+    int r0;        // L3 start relative to the 16-B aligned base
+    int nch;       // chunks to read
+    int fast_lo;   // first byte (rel) of the all-L4 region (16-B aligned)
+    int fast_hi;   // end (rel) of the all-L4 region (16-B aligned)
+    int l4lo, l4hi, fa;     // L4 range (rel) and L4 checksum field (rel), fa < -8 if none
+    int iplo, iphi;         // IPv4 header range (rel); empty if no IP sum
+    int pslo, pshi;         // pseudo-header address bytes (rel); empty if none
+};
+
+template <int TEAM, int U, bool VERIFY>
+__global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                              const uint4* __restrict__ desc, uint32_t n,
+                                              uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                              const uint8_t* __restrict__ flags_override,
+                                              uint8_t* __restrict__ arena_w) {
+    const int tl = threadIdx.x & (TEAM - 1);
+    const uint32_t team = (blockIdx.x * 256u + threadIdx.x) / TEAM;
+    const uint32_t nteams = gridDim.x * (256u / TEAM);
+
+    uint4 dnext = make_uint4(0, 0, 0, 0);
+    if (team < n) dnext = desc[team];
+
+    for (uint32_t p = team; p < n; p += nteams) {
+        const uint4 dv = dnext;
+        if (p + nteams < n) dnext = desc[p + nteams];   // prefetch the next descriptor
+
+        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        const int len = dv.z & 0xffff;
+        const int l4o = dv.z >> 16;
+        const int ver = dv.w & 0xff;
+        const int proto = (dv.w >> 8) & 0xff;
+        int fl = (dv.w >> 16) & 0xff;
+        if (flags_override) fl = flags_override[p];
+
+        // ---- validate (never read or write outside the arena) ----
+        bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
+        const bool raw = (fl & VPCSUM_F_RAW) != 0;
+        bool do_ip = false, do_l4 = false;
+        int fld = -1;
+        if (!bad && !raw) {
+            if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
+            else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
+            else bad = true;
+            if (!bad && (fl & VPCSUM_F_L4)) {
+                fld = l4_field(proto);
+                if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
+                else do_l4 = true;
+            }
+            if (!bad && (fl & VPCSUM_F_IP)) {
+                if (ver != 4) bad = true;
+                else do_ip = true;
+            }
+        }
+        if (bad) {
+            if (tl == 0) {
+                if (out) out[p] = 0;
+                if (status) status[p] = VPCSUM_S_BAD_DESC;
+            }
+            continue;
+        }
+
+        const uint8_t* l3 = arena + off;
+        const uint4* base = (const uint4*)((uintptr_t)l3 & ~(uintptr_t)15);
+        PktPlan pl;
+        pl.r0 = (int)((uintptr_t)l3 & 15);
+        const int need = (raw || do_l4) ? len : (do_ip ? l4o : 0);
+        pl.nch = (pl.r0 + need + 15) >> 4;
+        if (raw) {
+            pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
+            pl.fast_lo = (pl.r0 + 15) & ~15;
+        } else if (do_l4) {
+            pl.l4lo = pl.r0 + l4o; pl.l4hi = pl.r0 + len; pl.fa = pl.r0 + l4o + fld;
+            pl.fast_lo = (pl.fa + 2 + 15) & ~15;
+        } else {
+            pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
+            pl.fast_lo = 1 << 30;
+        }
+        pl.fast_hi = (pl.r0 + need) & ~15;
+        if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
+        if (do_l4 && proto != 1) {
+            pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
+            pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
+        } else { pl.pslo = 0; pl.pshi = 0; }
+
+        uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
+        uint32_t st_ip = 0, st_l4 = 0;   // stored fields (verify), as masked LE bytes
+
+        for (int r0 = 0; r0 * TEAM < pl.nch; r0 += U) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = (r0 + u) * TEAM + tl;
+                if (k < pl.nch) v[u] = base[k];
+                else v[u] = make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = (r0 + u) * TEAM + tl;
+                if (k >= pl.nch) continue;
+                const int c = k << 4;
+                if (c >= pl.fast_lo && c + 16 <= pl.fast_hi) {
+                    acc_l4 += (uint64_t)v[u].x + v[u].y;
+                    acc_l4 += (uint64_t)v[u].z + v[u].w;
+                } else {
+                    const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int d = c + 4 * j;
+                        const uint32_t mf = bmask(d, pl.fa, pl.fa + 2);
+                        acc_l4 += w[j] & bmask(d, pl.l4lo, pl.l4hi) & ~mf;
+                        const uint32_t mif = bmask(d, pl.r0 + 10, pl.r0 + 12);
+                        acc_ip += w[j] & bmask(d, pl.iplo, pl.iphi) & ~mif;
+                        acc_ps += w[j] & bmask(d, pl.pslo, pl.pshi);
+                        if (VERIFY) {
+                            st_l4 += w[j] & mf;
+                            st_ip += (w[j] & mif) & (do_ip ? 0xffffffffu : 0u);
+                        }
+                    }
+                }
+            }
+        }
+
+        uint32_t s_l4 = team_sum<TEAM>(fold64(acc_l4));
+        uint32_t s_ip = team_sum<TEAM>(fold64(acc_ip));
+        uint32_t s_ps = team_sum<TEAM>(fold64(acc_ps));
+        uint32_t s_stl4 = 0, s_stip = 0;
+        if (VERIFY) {
+            s_stl4 = team_sum<TEAM>(fold32(st_l4));
+            s_stip = team_sum<TEAM>(fold32(st_ip));
+        }
+
+        if (tl == 0) {
+            uint32_t ipc = 0, l4c = 0;
+            uint8_t st = VPCSUM_S_DONE;
+            if (raw) {
+                ipc = 0xffff - orient(fold32(s_l4), pl.r0);
+            } else {
+                if (do_ip) {
+                    ipc = 0xffff - orient(fold32(s_ip), pl.r0);
+                }
+                if (do_l4) {
+                    uint32_t tot = orient(fold32(s_l4), pl.r0 + l4o);
+                    if (proto != 1) {
+                        const uint32_t l4len = (uint32_t)(len - l4o);
+                        const int pproto = proto;   // Consts.IP_PROTOCOL_* of the L4 class
+                        tot += orient(fold32(s_ps), pl.r0) + (uint32_t)pproto + (l4len & 0xffff) + (l4len >> 16);
+                    }
+                    l4c = 0xffff - fold32(tot);
+                    if (proto == 17 && l4c == 0) l4c = 0xffff;
+                }
+                if (VERIFY) {
+                    if (do_ip && orient(fold32(s_stip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
+                    if (do_l4) {
+                        const uint32_t stored = orient(fold32(s_stl4), pl.fa);
+                        if (stored == l4c) st |= VPCSUM_S_L4_OK;
+                        if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                    }
+                }
+                if (arena_w) {
+                    uint8_t* w = arena_w + off;
+                    if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
+                    if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
+                }
+            }
+            if (out) out[p] = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
+            if (status) status[p] = st;
+        }
+    }
+}
+
+template <int TEAM, int U>
+static hipError_t launch_team(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
+                              uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify,
+                              uint8_t* arena_w, int grid, hipStream_t stream) {
+    const uint32_t per_block = 256 / TEAM;
+    uint32_t need = (n + per_block - 1) / per_block;
+    uint32_t g = grid > 0 ? (uint32_t)grid : need;
+    if (g > need) g = need;
+    if (g == 0) g = 1;
+    if (verify)
+        hipLaunchKernelGGL((k_csum<TEAM, U, true>), dim3(g), dim3(256), 0, stream, arena, arena_len,
+                           (const uint4*)desc, n, out, status, flags_override, arena_w);
+    else
+        hipLaunchKernelGGL((k_csum<TEAM, U, false>), dim3(g), dim3(256), 0, stream, arena, arena_len,
+                           (const uint4*)desc, n, out, status, flags_override, arena_w);
+    return hipGetLastError();
+}
+
+hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
+                       uint32_t* out, uint8_t* status, const uint8_t* flags_override, uint32_t mode,
+                       uint8_t* arena_w, int team_log2, int grid_override, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const bool verify = (mode & VPCSUM_MODE_VERIFY) != 0;
+    int grid = grid_override;
+    if (grid <= 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        grid = num_cus(dev) * 8;   // 8 blocks x 4 waves = 32 waves per CU
+    }
+    switch (team_log2) {
+        case 2: return launch_team<4, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, arena_w, grid, stream);
+        case 3: return launch_team<8, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, arena_w, grid, stream);
+        case 5: return launch_team<32, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, arena_w, grid, stream);
+        case 6: return launch_team<64, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, arena_w, grid, stream);
+        case 4:
+        default: return launch_team<16, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, arena_w, grid, stream);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// K5: NAT / TTL rewrite with RFC 1624 incremental update (one lane per packet).
+// Java writes the new bytes through the setters (Ipv4Packet.setSrc/setDst :433-458,
+// setTtl :401-407, TcpPacket/UdpPacket.setSrcPort/setDstPort) and recomputes the dirty sums
+// in full on the next getRawPacket(0) (SwitchUtils.applyNat, SwitchUtils.java:522-542).
+// RFC 1624 eqn. 3, HC' = ~(~HC + ~m + m'), is bit-identical to that full recompute whenever
+// the incoming checksum is correct; UDP with stored 0 is recomputed in full here.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ld16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+__device__ __forceinline__ void st16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+
+// Folded LE-absolute sum of bytes [lo, hi) (absolute addresses), one lane, aligned dwords.
+__device__ uint32_t lane_sum_range(const uint8_t* lo_p, const uint8_t* hi_p, const uint8_t* fld_p) {
+    const uintptr_t lo = (uintptr_t)lo_p, hi = (uintptr_t)hi_p, fa = (uintptr_t)fld_p;
+    const uintptr_t a = lo & ~(uintptr_t)3;
+    uint64_t acc = 0;
+    for (uintptr_t d = a; d < hi; d += 4) {
+        const uint32_t w = *(const uint32_t*)d;
+        const int rd = (int)(d - a);
+        uint32_t m = bmask(rd, (int)(lo - a), (int)(hi - a));
+        if (fld_p) m &= ~bmask(rd, (int)(fa - a), (int)(fa - a) + 2);
+        acc += w & m;
+    }
+    return fold64(acc);
+}
+
+__global__ __launch_bounds__(256) void k_nat4(uint8_t* __restrict__ arena, uint64_t arena_len,
+                                             const vpcsum_desc_t* __restrict__ desc,
+                                             const vpcsum_nat4_t* __restrict__ rw, uint32_t n,
+                                             uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out,
+                                             int strict) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+        const vpcsum_desc_t d = desc[p];
+        const vpcsum_nat4_t r = rw[p];
+        const uint64_t off = d.l3_off;
+        const int len = d.l3_len, l4o = d.l4_off;
+        if (off > arena_len || (uint64_t)len > arena_len - off || d.l3_ver != 4 || len < 20 || l4o < 20 ||
+            l4o > len || (l4o & 3)) {
+            if (status) status[p] = VPCSUM_S_BAD_DESC;
+            if (flags_out) flags_out[p] = kFlagRejected;
+            continue;
+        }
+        uint8_t* l3 = arena + off;
+        const int proto = d.l4_proto;
+        const int fld = (proto == 6 || proto == 17) ? l4_field(proto) : -1;
+        const bool l4 = fld >= 0 && len - l4o >= fld + 2;
+        uint8_t* l4p = l3 + l4o;
+
+        // old / new 16-bit words; ip: header words, ps: pseudo words (+ ports for l4)
+        uint32_t ip_diff = 0;   // sum of ~m + m' over changed IP header words
+        uint32_t l4_diff = 0;   // sum of ~m + m' over changed pseudo/L4 words
+        bool ip_dirty = false, l4_dirty = false;
+        if (r.mask & VPCSUM_NAT_SRC) {
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t m = ld16(l3 + 12 + 2 * i);
+                const uint32_t mn = ((uint32_t)r.src[2 * i] << 8) | r.src[2 * i + 1];
+                ip_diff += (~m & 0xffff) + mn;
+                l4_diff += (~m & 0xffff) + mn;
+                st16(l3 + 12 + 2 * i, mn);
+            }
+            ip_dirty = true; l4_dirty = true;
+        }
+        if (r.mask & VPCSUM_NAT_DST) {
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t m = ld16(l3 + 16 + 2 * i);
+                const uint32_t mn = ((uint32_t)r.dst[2 * i] << 8) | r.dst[2 * i + 1];
+                ip_diff += (~m & 0xffff) + mn;
+                l4_diff += (~m & 0xffff) + mn;
+                st16(l3 + 16 + 2 * i, mn);
+            }
+            ip_dirty = true; l4_dirty = true;
+        }
+        if (r.mask & VPCSUM_NAT_DEC_TTL) {
+            const uint32_t m = ld16(l3 + 8);
+            const uint32_t mn = (((m >> 8) - 1) & 0xff) << 8 | (m & 0xff);
+            ip_diff += (~m & 0xffff) + mn;
+            st16(l3 + 8, mn);
+            ip_dirty = true;
+        }
+        if (l4) {
+            if (r.mask & VPCSUM_NAT_SPORT) {
+                const uint32_t m = ld16(l4p);
+                const uint32_t mn = ((uint32_t)r.sport[0] << 8) | r.sport[1];
+                l4_diff += (~m & 0xffff) + mn;
+                st16(l4p, mn);
+                l4_dirty = true;
+            }
+            if (r.mask & VPCSUM_NAT_DPORT) {
+                const uint32_t m = ld16(l4p + 2);
+                const uint32_t mn = ((uint32_t)r.dport[0] << 8) | r.dport[1];
+                l4_diff += (~m & 0xffff) + mn;
+                st16(l4p + 2, mn);
+                l4_dirty = true;
+            }
+        } else {
+            l4_dirty = false;
+        }
+        uint8_t fl = (ip_dirty ? VPCSUM_F_IP : 0) | (l4_dirty ? VPCSUM_F_L4 : 0);
+        if (strict) {
+            // Java semantics for any input: the csum kernel recomputes the dirty sums in full.
+            if (flags_out) flags_out[p] = fl;
+            continue;
+        }
+        if (ip_dirty) {
+            const uint32_t hc = ld16(l3 + 10);
+            const uint32_t s = fold32((~hc & 0xffff) + fold32(ip_diff));
+            st16(l3 + 10, ~s & 0xffff);
+        }
+        if (l4_dirty) {
+            const uint32_t hc = ld16(l4p + fld);
+            uint32_t c;
+            if (proto == 17 && hc == 0) {
+                // "no checksum" UDP: Java recomputes the full sum (UdpPacket.java:136-149)
+                const uint32_t seg = orient(lane_sum_range(l4p, l3 + len, l4p + fld), (int)((uintptr_t)l4p & 1));
+                const uint32_t ps = orient(lane_sum_range(l3 + 12, l3 + 20, nullptr), (int)((uintptr_t)l3 & 1));
+                const uint32_t l4len = (uint32_t)(len - l4o);
+                c = 0xffff - fold32(seg + ps + 17u + l4len);
+            } else {
+                const uint32_t s = fold32((~hc & 0xffff) + fold32(l4_diff));
+                c = ~s & 0xffff;
+            }
+            if (proto == 17 && c == 0) c = 0xffff;
+            st16(l4p + fld, c);
+        }
+        if (status) status[p] = VPCSUM_S_DONE;
+    }
+}
+
+hipError_t launch_nat4(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const vpcsum_nat4_t* rw,
+                       uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    uint32_t g = (n + 255) / 256;
+    uint32_t cap = (uint32_t)num_cus(dev) * 8;
+    if (g > cap) g = cap;
+    hipLaunchKernelGGL(k_nat4, dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out,
+                       (int)(nat_mode & VPCSUM_NAT_STRICT_JAVA));
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Parse kernel (one lane per frame): EthernetPacket.from (EthernetPacket.java:25-94) ->
+// Ipv4Packet.from (Ipv4Packet.java:73-145) / Ipv6Packet.from (Ipv6Packet.java:69-159),
+// reduced to what the checksum needs.  IPv6 extension headers follow the reference's
+// ExtHeader.from (Ipv6Packet.java ExtHeader: 8 + hdrExtLen bytes); a chain of two or more
+// makes the reference loop forever, so such frames are rejected.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool v6_needs_next(int h) {
+    return h == 0 || h == 60 || h == 43 || h == 44 || h == 51 || h == 50 || h == 135 || h == 139 || h == 140 ||
+           h == 253 || h == 254;
+}
+
+__global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                    const uint64_t* __restrict__ foff,
+                                                    const uint32_t* __restrict__ flen, uint32_t n, uint8_t want,
+                                                    vpcsum_desc_t* __restrict__ desc, uint8_t* __restrict__ status) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+        const uint64_t o = foff[p];
+        uint32_t L = flen[p];
+        vpcsum_desc_t d;
+        d.l3_off = 0; d.l3_len = 0; d.l4_off = 0; d.l3_ver = 0; d.l4_proto = 0; d.flags = 0; d.rsv = 0;
+        uint8_t st = VPCSUM_S_BAD_DESC;
+        bool ok = o <= arena_len && (uint64_t)L <= arena_len - o && L >= 14;
+        const uint8_t* f = arena + o;
+        int hl = 14, typ = 0;
+        if (ok) {
+            typ = ld16(f + 12);
+            if (typ == 0x8100) {
+                if (L < 18) ok = false;
+                else { typ = ld16(f + 16); hl = 18; }
+            }
+            ok = ok && (typ == 0x0800 || typ == 0x86DD);
+        }
+        if (ok) {
+            const uint8_t* b = f + hl;
+            const uint32_t avail = L - hl;
+            const int ver = avail >= 1 ? (b[0] >> 4) : 0;
+            if (typ == 0x0800 && ver == 4 && avail >= 20) {
+                const int ihl = b[0] & 15;
+                const uint32_t total = ld16(b + 2);
+                if (avail >= (uint32_t)ihl * 4 && ihl >= 5 && total >= (uint32_t)ihl * 4 && total <= avail) {
+                    d.l3_off = o + hl; d.l3_len = (uint16_t)total; d.l4_off = (uint16_t)(ihl * 4);
+                    d.l3_ver = 4; d.l4_proto = b[9];
+                    st = 0;
+                }
+            } else if (typ == 0x86DD && ver == 6 && avail >= 40) {
+                const uint32_t pl = ld16(b + 4);
+                const int nh = b[6];
+                if (pl != 0 && 40 + pl <= avail) {
+                    const uint32_t total = 40 + pl;
+                    int proto = nh, l4o = 40;
+                    bool good = true;
+                    if (v6_needs_next(nh)) {
+                        if (total - 40 < 8) good = false;
+                        else {
+                            const int nxt = b[40], hlen = b[41];
+                            if (total - 40 < (uint32_t)(8 + hlen) || v6_needs_next(nxt)) good = false;
+                            else { proto = nxt; l4o = 40 + 8 + hlen; }
+                        }
+                    }
+                    if (good && total <= 0xffff) {
+                        d.l3_off = o + hl; d.l3_len = (uint16_t)total; d.l4_off = (uint16_t)l4o;
+                        d.l3_ver = 6; d.l4_proto = (uint8_t)proto;
+                        st = 0;
+                    }
+                }
+            }
+        }
+        if (st == 0) {
+            uint8_t fl = 0;
+            if ((want & VPCSUM_F_IP) && d.l3_ver == 4) fl |= VPCSUM_F_IP;
+            const int fld = l4_field(d.l4_proto);
+            if ((want & VPCSUM_F_L4) && fld >= 0 && !(d.l3_ver == 4 && d.l4_proto == 58) &&
+                d.l3_len - d.l4_off >= fld + 2)
+                fl |= VPCSUM_F_L4;
+            d.flags = fl;
+        }
+        desc[p] = d;
+        if (status) status[p] = st;
+    }
+}
+
+hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const uint64_t* frame_off,
+                              const uint32_t* frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* desc,
+                              uint8_t* status, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    uint32_t g = (n + 255) / 256;
+    if (g > 65535u * 8) g = 65535u * 8;
+    hipLaunchKernelGGL(k_parse_ether, dim3(g), dim3(256), 0, stream, arena, arena_len, frame_off, frame_len, n,
+                       flags, desc, status);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Read-roof probe: plain streaming dwordx4 read of `bytes`, XOR-reduced per block.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_read_probe(const uint4* __restrict__ buf, uint64_t n16,
+                                                   uint32_t* __restrict__ sink) {
+    uint32_t x = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = buf[i], b = buf[i + stride], c = buf[i + 2 * stride], d = buf[i + 3 * stride];
+        x ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    }
+    for (; i < n16; i += stride) {
+        const uint4 a = buf[i];
+        x ^= a.x ^ a.y ^ a.z ^ a.w;
+    }
+    for (int m = 32; m >= 1; m >>= 1) x ^= __shfl_xor(x, m, 64);
+    if ((threadIdx.x & 63) == 0) atomicXor(&sink[blockIdx.x], x);
+}
+
+hipError_t launch_read_probe(const uint8_t* buf, uint64_t bytes, uint32_t* sink, uint32_t grid, hipStream_t stream) {
+    if (grid == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        grid = num_cus(dev) * 8;
+    }
+    hipLaunchKernelGGL(k_read_probe, dim3(grid), dim3(256), 0, stream, (const uint4*)buf, bytes / 16, sink);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Synthetic workload generator: same bytes as oracle/csum_oracle.c:orc_synth_frame.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t rng(uint64_t seed, uint64_t pkt, uint64_t word) {
+    const uint64_t ctr = (pkt << 20) | (word & 0xFFFFFull);
+    return mix64(seed + (ctr + 1) * 0x9E3779B97F4A7C15ull);
+}
+
+struct Shape { int ver, proto, l3_len, l4_off; };
+
+__device__ Shape shape_of(uint32_t workload, uint64_t seed, uint64_t pkt) {
+    Shape s = {4, 6, 1500, 20};
+    const uint64_t r = rng(seed, pkt, 0xFFFFF);
+    switch (workload) {
+        case VPCSUM_SYNTH_C1_UDP64: s.proto = 17; s.l3_len = 50; break;
+        case VPCSUM_SYNTH_C2_TCP1500: break;
+        case VPCSUM_SYNTH_C3_MIXED: {
+            const int lens[3] = {64, 576, 1500};
+            const int protos[3] = {17, 6, 1};
+            s.l3_len = lens[r % 3];
+            s.proto = protos[(r / 3) % 3];
+            break;
+        }
+        case VPCSUM_SYNTH_C4_V6JUMBO: s.ver = 6; s.proto = 6; s.l3_len = 9000; s.l4_off = 40; break;
+        default: {
+            const int protos4[4] = {6, 17, 1, 6};
+            const int protos6[4] = {6, 17, 58, 17};
+            s.ver = (r & 1) ? 6 : 4;
+            if (s.ver == 4) {
+                s.proto = protos4[(r >> 1) & 3];
+                s.l4_off = 20 + 4 * (int)((r >> 3) % 11);
+            } else {
+                s.proto = protos6[(r >> 1) & 3];
+                s.l4_off = 40;
+            }
+            const int minl4 = (s.proto == 6) ? 20 : 8;
+            uint32_t span = 1600;
+            if (((r >> 8) & 15) == 0) span = 9000;
+            s.l3_len = s.l4_off + minl4 + (int)((r >> 12) % span);
+            if (s.l3_len > 9000) s.l3_len = 9000;
+            if (((r >> 40) & 63) == 0) s.l3_len = s.l4_off + minl4;
+            break;
+        }
+    }
+    return s;
+}
+
+// One block per packet: threads fill the payload 8 bytes at a time, then thread 0 writes
+// the header fields (same order as the oracle: payload first, headers overwrite).
+__global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ arena, uint32_t n, uint32_t stride,
+                                              uint32_t l3_pad, uint32_t workload, uint64_t seed,
+                                              uint64_t first, vpcsum_desc_t* __restrict__ desc) {
+    for (uint32_t p = blockIdx.x; p < n; p += gridDim.x) {
+        const uint64_t pkt = first + p;
+        const Shape s = shape_of(workload, seed, pkt);
+        uint8_t* l3 = arena + (uint64_t)p * stride + l3_pad;
+        const int nw = (s.l3_len + 7) >> 3;
+        for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+            const uint64_t v = rng(seed, pkt, (uint64_t)w);
+            const int b0 = w * 8;
+            if ((((uintptr_t)(l3 + b0)) & 7) == 0 && b0 + 8 <= s.l3_len) {
+                *(uint64_t*)(l3 + b0) = v;
+            } else {
+                for (int b = 0; b < 8 && b0 + b < s.l3_len; ++b) l3[b0 + b] = (uint8_t)(v >> (8 * b));
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (s.ver == 4) {
+                l3[0] = (uint8_t)(0x40 | (s.l4_off / 4));
+                l3[1] = 0;
+                l3[2] = (uint8_t)(s.l3_len >> 8); l3[3] = (uint8_t)s.l3_len;
+                l3[6] = 0x40; l3[7] = 0;
+                l3[8] = 64; l3[9] = (uint8_t)s.proto;
+                l3[10] = 0; l3[11] = 0;
+            } else {
+                const int pl = s.l3_len - 40;
+                l3[0] = 0x60; l3[1] &= 0x0f;
+                l3[4] = (uint8_t)(pl >> 8); l3[5] = (uint8_t)pl;
+                l3[6] = (uint8_t)s.proto; l3[7] = 64;
+            }
+            uint8_t* l4 = l3 + s.l4_off;
+            const int l4len = s.l3_len - s.l4_off;
+            if (s.proto == 6) {
+                l4[12] = 0x50; l4[13] = 0x10; l4[16] = 0; l4[17] = 0; l4[18] = 0; l4[19] = 0;
+            } else if (s.proto == 17) {
+                l4[4] = (uint8_t)(l4len >> 8); l4[5] = (uint8_t)l4len; l4[6] = 0; l4[7] = 0;
+            } else {
+                l4[0] = (s.proto == 58) ? 128 : 8; l4[1] = 0; l4[2] = 0; l4[3] = 0;
+            }
+            if (desc) {
+                vpcsum_desc_t d;
+                d.l3_off = (uint64_t)p * stride + l3_pad;
+                d.l3_len = (uint16_t)s.l3_len;
+                d.l4_off = (uint16_t)s.l4_off;
+                d.l3_ver = (uint8_t)s.ver;
+                d.l4_proto = (uint8_t)s.proto;
+                d.flags = (uint8_t)((s.ver == 4 ? VPCSUM_F_IP : 0) | VPCSUM_F_L4);
+                d.rsv = 0;
+                desc[p] = d;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_synth(uint8_t* arena, uint64_t arena_len, uint32_t n, uint32_t stride, uint32_t l3_pad,
+                        uint32_t workload, uint64_t seed, uint64_t first_index, vpcsum_desc_t* desc,
+                        hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    uint32_t g = n < 65536u ? n : 65536u;
+    hipLaunchKernelGGL(k_synth, dim3(g), dim3(256), 0, stream, arena, n, stride, l3_pad, workload, seed,
+                       first_index, desc);
+    return hipGetLastError();
+}
+
+}  // namespace vpcsum

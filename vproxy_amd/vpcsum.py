@@ -1,0 +1,248 @@
+"""ctypes binding of libvpcsum.so (C-ABI in include/vpcsum.h) plus the host-side helpers the
+vswitch mirror and the tests use.
+
+There is deliberately NO CPU fallback: if the HIP library cannot be loaded, every entry point
+raises :class:`VpcsumUnavailable`.  Device memory and streams come from PyTorch (plumbing only);
+``import torch`` happens before the library is loaded so that libvpcsum binds to the same HIP
+runtime instance as torch (both carry SONAME libamdhip64.so.7).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from .build import LIB
+
+F_IP, F_L4, F_RAW = 0x01, 0x02, 0x04
+S_IP_OK, S_L4_OK, S_UDP_NOCSUM, S_DONE, S_BAD_DESC = 0x01, 0x02, 0x04, 0x40, 0x80
+MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
+NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL = 0x01, 0x02, 0x04, 0x08, 0x10
+NAT_RFC1624, NAT_STRICT_JAVA = 0x00, 0x01
+SYNTH_C1, SYNTH_C2, SYNTH_C3, SYNTH_C4, SYNTH_FUZZ = 1, 2, 3, 4, 5
+
+DESC_DTYPE = np.dtype([("l3_off", "<u8"), ("l3_len", "<u2"), ("l4_off", "<u2"), ("l3_ver", "u1"),
+                       ("l4_proto", "u1"), ("flags", "u1"), ("rsv", "u1")])
+NAT4_DTYPE = np.dtype([("src", "u1", 4), ("dst", "u1", 4), ("sport", "u1", 2), ("dport", "u1", 2),
+                       ("mask", "u1"), ("rsv", "u1", 3)])
+
+# Every symbol include/vpcsum.h declares (tests check the .so exports all of them).
+EXPORTS = [
+    "vpcsum_abi_version", "vpcsum_last_error", "vpcsum_device_count", "vpcsum_set_device",
+    "vpcsum_compute_async", "vpcsum_nat4_async", "vpcsum_parse_ether_async", "vpcsum_read_probe_async",
+    "vpcsum_synth_async", "vpcsum_event_create", "vpcsum_event_destroy", "vpcsum_event_record",
+    "vpcsum_event_elapsed_ms", "vpcsum_stream_sync", "vpcsum_ctx_create", "vpcsum_ctx_destroy",
+    "vpcsum_ctx_register_arena", "vpcsum_ctx_unregister_arena", "vpcsum_ctx_submit", "vpcsum_ctx_wait",
+    "vpcsum_ctx_pipeline",
+    "Java_io_vproxy_vpcsum_VPCsum_create", "Java_io_vproxy_vpcsum_VPCsum_registerArena",
+    "Java_io_vproxy_vpcsum_VPCsum_submit", "Java_io_vproxy_vpcsum_VPCsum_waitFor",
+    "Java_io_vproxy_vpcsum_VPCsum_close",
+]
+
+
+class VpcsumUnavailable(RuntimeError):
+    pass
+
+
+class VpcsumError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _declare(L):
+    P, I, U8, U32, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64
+    sig = {
+        "vpcsum_abi_version": ([], I),
+        "vpcsum_last_error": ([], ctypes.c_char_p),
+        "vpcsum_device_count": ([P], I),
+        "vpcsum_set_device": ([I], I),
+        "vpcsum_compute_async": ([P, U64, P, U32, P, P, U32, P], I),
+        "vpcsum_nat4_async": ([P, U64, P, P, U32, P, U32, P], I),
+        "vpcsum_parse_ether_async": ([P, U64, P, P, U32, U8, P, P, P], I),
+        "vpcsum_read_probe_async": ([P, U64, P, U32, P], I),
+        "vpcsum_synth_async": ([P, U64, U32, U32, U32, U32, U64, U64, P, P], I),
+        "vpcsum_event_create": ([P], I),
+        "vpcsum_event_destroy": ([P], I),
+        "vpcsum_event_record": ([P, P], I),
+        "vpcsum_event_elapsed_ms": ([P, P, P], I),
+        "vpcsum_stream_sync": ([P], I),
+        "vpcsum_ctx_create": ([I, U64, U32, P], I),
+        "vpcsum_ctx_destroy": ([P], I),
+        "vpcsum_ctx_register_arena": ([P, P, U64], I),
+        "vpcsum_ctx_unregister_arena": ([P, P], I),
+        "vpcsum_ctx_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
+        "vpcsum_ctx_wait": ([P, U64], I),
+        "vpcsum_ctx_pipeline": ([P, P, U32, U32, P, U32, P, U32, U32], I),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+
+
+def lib():
+    """Load libvpcsum.so (after torch, so both share one HIP runtime)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB):
+                raise VpcsumUnavailable(f"{LIB} is missing: run `python -m vproxy_amd.build` "
+                                        "(there is no CPU fallback)")
+            try:
+                import torch  # noqa: F401  -- bind torch's libamdhip64 first
+            except ImportError:
+                pass
+            try:
+                L = ctypes.CDLL(LIB)
+            except OSError as e:
+                raise VpcsumUnavailable(f"cannot load {LIB}: {e}") from e
+            _declare(L)
+            if L.vpcsum_abi_version() != 1:
+                raise VpcsumUnavailable("ABI version mismatch")
+            _lib = L
+        return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().vpcsum_last_error()
+        raise VpcsumError(f"{what}: {msg.decode() if msg else rc}")
+
+
+def _ptr(t) -> int | None:
+    if t is None:
+        return None
+    if isinstance(t, np.ndarray):
+        return t.ctypes.data
+    return t.data_ptr()
+
+
+def _stream(stream) -> int | None:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+# ------------------------------------------------------------------------------------------
+# Device-resident API (torch CUDA tensors)
+# ------------------------------------------------------------------------------------------
+def compute(arena, desc, n: int | None = None, out=None, status=None, mode: int = MODE_COMPUTE,
+            team_log2: int = 0, stream=None):
+    """Checksum a device-resident batch.  `arena` uint8 tensor, `desc` tensor holding n
+    16-byte vpcsum_desc_t, `out` int32/uint32 tensor (n), `status` uint8 tensor (n)."""
+    if n is None:
+        n = desc.numel() * desc.element_size() // 16
+    m = mode | ((team_log2 & 0xF) << 8)
+    _check(lib().vpcsum_compute_async(_ptr(arena), arena.numel(), _ptr(desc), n, _ptr(out), _ptr(status), m,
+                                      _stream(stream)), "vpcsum_compute_async")
+
+
+def nat4(arena, desc, rw, n: int, status=None, nat_mode: int = NAT_RFC1624, stream=None):
+    _check(lib().vpcsum_nat4_async(_ptr(arena), arena.numel(), _ptr(desc), _ptr(rw), n, _ptr(status), nat_mode,
+                                   _stream(stream)), "vpcsum_nat4_async")
+
+
+def parse_ether(arena, frame_off, frame_len, n: int, desc, status=None, flags: int = F_IP | F_L4, stream=None):
+    _check(lib().vpcsum_parse_ether_async(_ptr(arena), arena.numel(), _ptr(frame_off), _ptr(frame_len), n, flags,
+                                          _ptr(desc), _ptr(status), _stream(stream)), "vpcsum_parse_ether_async")
+
+
+def read_probe(buf, nbytes: int, sink, grid: int = 0, stream=None):
+    _check(lib().vpcsum_read_probe_async(_ptr(buf), nbytes, _ptr(sink), grid, _stream(stream)),
+           "vpcsum_read_probe_async")
+
+
+def synth(arena, n: int, stride: int, l3_pad: int, workload: int, seed: int, first_index: int = 0,
+          desc=None, stream=None):
+    _check(lib().vpcsum_synth_async(_ptr(arena), arena.numel(), n, stride, l3_pad, workload, seed, first_index,
+                                    _ptr(desc), _stream(stream)), "vpcsum_synth_async")
+
+
+class Event:
+    """HIP event recorded on an arbitrary (e.g. the kernel's) stream."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        _check(lib().vpcsum_event_create(ctypes.byref(h)), "vpcsum_event_create")
+        self.h = h.value
+
+    def record(self, stream=None):
+        _check(lib().vpcsum_event_record(self.h, _stream(stream)), "vpcsum_event_record")
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = ctypes.c_float()
+        _check(lib().vpcsum_event_elapsed_ms(self.h, end.h, ctypes.byref(ms)), "vpcsum_event_elapsed_ms")
+        return ms.value
+
+    def __del__(self):
+        try:
+            if _lib is not None and self.h:
+                _lib.vpcsum_event_destroy(self.h)
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------------------------------
+# Host-memory API (what the Java binding drives)
+# ------------------------------------------------------------------------------------------
+class Context:
+    def __init__(self, device: int = 0, max_arena: int = 1 << 26, max_pkts: int = 1 << 16):
+        h = ctypes.c_void_p()
+        _check(lib().vpcsum_ctx_create(device, max_arena, max_pkts, ctypes.byref(h)), "vpcsum_ctx_create")
+        self.h = h.value
+
+    def register(self, arr: np.ndarray):
+        _check(lib().vpcsum_ctx_register_arena(self.h, arr.ctypes.data, arr.nbytes), "vpcsum_ctx_register_arena")
+
+    def unregister(self, arr: np.ndarray):
+        _check(lib().vpcsum_ctx_unregister_arena(self.h, arr.ctypes.data), "vpcsum_ctx_unregister_arena")
+
+    def submit(self, arena: np.ndarray, desc: np.ndarray, out: np.ndarray, status: np.ndarray | None = None,
+               mode: int = MODE_COMPUTE) -> int:
+        t = ctypes.c_uint64()
+        _check(lib().vpcsum_ctx_submit(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data, len(desc),
+                                       out.ctypes.data, None if status is None else status.ctypes.data, mode,
+                                       ctypes.byref(t)), "vpcsum_ctx_submit")
+        return t.value
+
+    def wait(self, ticket: int):
+        _check(lib().vpcsum_ctx_wait(self.h, ticket), "vpcsum_ctx_wait")
+
+    def run(self, arena, desc, mode: int = MODE_COMPUTE):
+        out = np.zeros(len(desc), np.uint32)
+        status = np.zeros(len(desc), np.uint8)
+        self.wait(self.submit(arena, desc, out, status, mode))
+        return out, status
+
+    def pipeline(self, arena: np.ndarray, stride: int, copy_bytes: int, desc: np.ndarray, out: np.ndarray,
+                 mode: int = MODE_COMPUTE, chunks: int = 8):
+        _check(lib().vpcsum_ctx_pipeline(self.h, arena.ctypes.data, stride, copy_bytes, desc.ctypes.data, len(desc),
+                                         out.ctypes.data, mode, chunks), "vpcsum_ctx_pipeline")
+
+    def close(self):
+        if self.h:
+            lib().vpcsum_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def desc_to_tensor(desc: np.ndarray, device="cuda"):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(desc).view(np.uint8).copy()).to(device)
+
+
+def tensor_to_desc(t) -> np.ndarray:
+    return t.cpu().numpy().view(DESC_DTYPE).copy()
