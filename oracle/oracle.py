@@ -249,6 +249,8 @@ class Oracle:
         n = len(desc)
         out = np.zeros(n, np.uint32)
         status = np.zeros(n, np.uint8)
+        if write:
+            mode |= MODE_WRITE
         if threads > 1 and not write:
             rc = self.L.orc_process_batch_mt(self._p(arena), arena.nbytes, self._p(desc), n, mode,
                                              self._p(out), self._p(status), threads)
