@@ -72,7 +72,7 @@ def pack(frames, infos, stride=None, pad=0):
 
 
 @pytest.mark.parametrize("pad", [0, 1, 2, 3, 14, 15, 398])
-@pytest.mark.parametrize("team", [0, 2, 3, 5, 6])
+@pytest.mark.parametrize("team", [0, 2, 3, 5, 6, 9, 12, 16, 17, 21, 22, 26, 28, 29])
 def test_kats_on_gpu(V, orc, pad, team):
     kats, frames, infos = kat_batch()
     arena, desc = pack(frames, infos, pad=pad)
@@ -129,7 +129,7 @@ def test_synth_matches_oracle_and_checksums(V, orc, workload, pad):
     torch.cuda.synchronize()
     assert np.array_equal(arena.cpu().numpy(), arena_o), "GPU generator differs from oracle generator"
     assert np.array_equal(V.tensor_to_desc(d), desc_o)
-    for team in (0, 2, 6):
+    for team in (0, 2, 6, 12, 16, 21, 26, 29):
         out, st, written = gpu_compute(V, arena_o, desc_o, O.MODE_COMPUTE, team, write=True)
         a2 = arena_o.copy()
         oout, ost = orc.process(a2, desc_o, O.MODE_COMPUTE, write=True)
@@ -363,3 +363,19 @@ def test_full_size_c2_properties(V, orc):
         a1, d1 = orc.synth(1, stride, 0, O.SYNTH_C2, O.SEED, int(i))
         w, _ = orc.process(a1, d1)
         assert o[i] == w[0]
+
+
+@pytest.mark.parametrize("team", [0, 3, 9, 21, 26])
+def test_packet_ending_at_unaligned_arena_end(V, orc, team):
+    """Arena length not a multiple of 16 and the last packet ending exactly at the arena end:
+    the final partial chunk must still be read (buffer-descriptor range rounding)."""
+    kats, frames, infos = kat_batch()
+    for fr, inf in zip(frames, infos):
+        for pad in (0, 1, 5, 14):
+            arena = np.zeros(pad + len(fr), np.uint8)
+            arena[pad:] = np.frombuffer(fr, np.uint8)
+            rows = [(pad + x.l3_off, x.l3_len, x.l4_off, x.ver, x.proto, O.desc_flags_for(x), 0) for x in inf]
+            desc = np.array(rows, dtype=O.DESC_DTYPE)
+            out, st, _ = gpu_compute(V, arena, desc, O.MODE_VERIFY, team)
+            oout, ost = orc.process(arena, desc, O.MODE_VERIFY)
+            assert np.array_equal(out, oout) and np.array_equal(st, ost), (pad, len(fr))

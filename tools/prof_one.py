@@ -1,0 +1,22 @@
+"""Run one checksum-kernel variant a few times (for rocprofv3 --pmc / --kernel-trace)."""
+import argparse, os, sys
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vproxy_amd import vpcsum as V
+from bench import WORKLOADS
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="c2")
+ap.add_argument("--variants", default="0")
+ap.add_argument("--bpc", type=int, default=0)
+ap.add_argument("--iters", type=int, default=5)
+a = ap.parse_args()
+sid, n, stride, _ = WORKLOADS[a.workload]
+arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+V.synth(arena, n, stride, 0, sid, 0x20241020, 0, d)
+out = torch.zeros(n, dtype=torch.int32, device="cuda")
+for v in map(int, a.variants.split(",")):
+    for _ in range(a.iters):
+        V.compute(arena, d, n, out, None, 0, v, blocks_per_cu=a.bpc)
+torch.cuda.synchronize()
+print("done")

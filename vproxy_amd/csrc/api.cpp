@@ -113,16 +113,23 @@ int vpcsum_set_device(int device) {
     return 0;
 }
 
-static int team_from_mode(uint32_t mode) { return (int)((mode >> 8) & 0xf); }
+static int team_from_mode(uint32_t mode) { return (int)((mode >> 8) & 0x1f); }
 
 int vpcsum_compute_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, uint32_t n,
                          uint32_t* d_out, uint8_t* d_status, uint32_t mode, void* stream) {
     if (n == 0) return 0;
     if (!d_arena || !d_desc) return fail("vpcsum_compute_async: NULL arena or descriptors");
-    if (mode & ~(0xfffu | VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_compute_async: bad mode 0x%x", mode);
+    // tuning hints (not part of the stable ABI): bits 8..12 kernel variant, bit 13 plain
+    // (temporal) loads, bits 16..23 workgroups per CU.
+    if (mode & ~(0x00ff3fffu | VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_compute_async: bad mode 0x%x", mode);
     uint8_t* w = (mode & VPCSUM_MODE_WRITE) ? const_cast<uint8_t*>(d_arena) : nullptr;
-    // bits 12..27 of the mode word are unused; bits 8..11 = log2(lanes per packet) tuning hint
-    VPC_CHECK(launch_csum(d_arena, arena_len, d_desc, n, d_out, d_status, nullptr, mode, w, team_from_mode(mode), 0,
+    int grid = 0;
+    if ((mode >> 16) & 0xff) {
+        int dev = 0;
+        VPC_CHECK(hipGetDevice(&dev), "hipGetDevice");
+        grid = num_cus(dev) * (int)((mode >> 16) & 0xff);
+    }
+    VPC_CHECK(launch_csum(d_arena, arena_len, d_desc, n, d_out, d_status, nullptr, mode, w, team_from_mode(mode), grid,
                           (hipStream_t)stream),
               "vpcsum_compute_async launch");
     return 0;

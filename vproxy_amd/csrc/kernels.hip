@@ -36,6 +36,26 @@ __device__ __forceinline__ uint32_t bmask(int d, int lo, int hi) {
     return me & ~ms;
 }
 
+// Bytes of the dword at relative position d that lie before `hi`.
+__device__ __forceinline__ uint32_t tailmask(int d, int hi) {
+    const int e = min(max(hi - d, 0), 4);
+    return e >= 4 ? 0xffffffffu : ((1u << (e << 3)) - 1u);
+}
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// Packet bytes are read exactly once: non-temporal loads keep them from displacing the
+// descriptors and the next packets' lines in L2 / MALL (measured +10% on this pattern,
+// tools/bwlab.hip).
+// (address space 1 so hipcc emits global_load_dwordx4, not flat_load: flat loads count on
+// lgkmcnt too and force vmcnt(0)+lgkmcnt(0) waits that serialise the U loads in flight.)
+typedef __attribute__((address_space(1))) const u32x4_t gu32x4_t;
+template <bool NT>
+__device__ __forceinline__ uint4 ld_stream(const uint4* q) {
+    const u32x4_t v = NT ? __builtin_nontemporal_load((gu32x4_t*)q) : *(gu32x4_t*)q;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // End-around-carry fold of a 64-bit sum of LE words to 16 bits; 0 only for 0.
 __device__ __forceinline__ uint32_t fold64(uint64_t x) {
     uint64_t t = (x & 0xffffffffull) + (x >> 32);
@@ -62,6 +82,12 @@ __device__ __forceinline__ int l4_field(int proto) {
 // per-packet dirty flags to the checksum kernel through flags_override).
 constexpr int kFlagRejected = 0x80;
 
+// Default lanes per packet.  Per-packet work (descriptor decode, header masks, team reduction,
+// result write) is issued once per wave for 64/TEAM packets, so small teams amortise it;
+// the payload loop costs the same per byte for any TEAM.
+constexpr int kDefaultTeam = 8;
+constexpr int kDefaultUnroll = 12;
+
 template <int TEAM>
 __device__ __forceinline__ uint32_t team_sum(uint32_t v) {
 #pragma unroll
@@ -86,7 +112,7 @@ struct PktPlan {
     int pslo, pshi;         // pseudo-header address bytes (rel); empty if none
 };
 
-template <int TEAM, int U, bool VERIFY>
+template <int TEAM, int U, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                               const uint4* __restrict__ desc, uint32_t n,
                                               uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -97,11 +123,19 @@ __global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena,
     const uint32_t nteams = gridDim.x * (256u / TEAM);
 
     uint4 dnext = make_uint4(0, 0, 0, 0);
-    if (team < n) dnext = desc[team];
+    int fnext = 0;
+    if (team < n) {
+        dnext = desc[team];
+        if (flags_override) fnext = flags_override[team];
+    }
 
     for (uint32_t p = team; p < n; p += nteams) {
         const uint4 dv = dnext;
-        if (p + nteams < n) dnext = desc[p + nteams];   // prefetch the next descriptor
+        const int fov = fnext;
+        if (p + nteams < n) {   // prefetch the next descriptor while this packet streams
+            dnext = desc[p + nteams];
+            if (flags_override) fnext = flags_override[p + nteams];
+        }
 
         const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
         const int len = dv.z & 0xffff;
@@ -109,7 +143,7 @@ __global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena,
         const int ver = dv.w & 0xff;
         const int proto = (dv.w >> 8) & 0xff;
         int fl = (dv.w >> 16) & 0xff;
-        if (flags_override) fl = flags_override[p];
+        if (flags_override) fl = fov;
 
         // ---- validate (never read or write outside the arena) ----
         bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
@@ -168,9 +202,10 @@ __global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena,
             uint4 v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int k = (r0 + u) * TEAM + tl;
-                if (k < pl.nch) v[u] = base[k];
-                else v[u] = make_uint4(0, 0, 0, 0);
+                // unconditional load (index clamped to the last chunk, a cache hit) keeps the
+                // U loads branch-free and in flight together; out-of-range chunks are skipped below
+                const int k = min((r0 + u) * TEAM + tl, pl.nch - 1);
+                v[u] = ld_stream<NT>(base + k);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -178,9 +213,16 @@ __global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena,
                 if (k >= pl.nch) continue;
                 const int c = k << 4;
                 if (c >= pl.fast_lo && c + 16 <= pl.fast_hi) {
+                    // payload chunk: every byte belongs to the L4 sum
                     acc_l4 += (uint64_t)v[u].x + v[u].y;
                     acc_l4 += (uint64_t)v[u].z + v[u].w;
+                } else if (c >= pl.fast_lo) {
+                    // tail chunk: past the header and the checksum field, only the end is cut
+                    const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
                 } else {
+                    // header chunk: IPv4 header / pseudo addresses / L4 header / fields
                     const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -247,21 +289,911 @@ __global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena,
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// K1b: "wave" form of the checksum kernel.  A wave owns 64 consecutive packets per iteration:
+//   * per-packet work is lane-parallel -- lane i decodes descriptor i (one coalesced 1 KiB
+//     load), walks packet i's header chunks (IPv4 header, pseudo addresses, L4 header, the
+//     checksum fields: the byte-masked work), and writes result i (coalesced stores);
+//   * the payload (16-B chunks from the first chunk after the L4 checksum field to the end) is
+//     streamed by teams of TEAM lanes, 64/TEAM packets at a time, fast path + one masked tail;
+//     each team's sum is handed to the packet's lane with one shuffle.
+// So the masked header work is issued once per 64 packets instead of once per 64/TEAM.
+// ------------------------------------------------------------------------------------------
+template <int TEAM, int U, int UH, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) void k_csum_wave(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   const uint4* __restrict__ desc, uint32_t n,
+                                                   uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                                   const uint8_t* __restrict__ flags_override,
+                                                   uint8_t* __restrict__ arena_w) {
+    constexpr int PPS = 64 / TEAM;   // packets per payload sub-iteration
+    const int lane = threadIdx.x & 63;
+    const int tl = lane & (TEAM - 1);
+    const int tid = lane / TEAM;
+    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t nwaves = gridDim.x * 4u;
+
+    for (uint32_t pbase = wave * 64u; pbase < n; pbase += nwaves * 64u) {
+        const uint32_t p = pbase + lane;
+        const bool live = p < n;
+        uint4 dv = make_uint4(0, 0, 0, 0);
+        int fl = 0;
+        if (live) {
+            dv = desc[p];
+            fl = flags_override ? flags_override[p] : (int)((dv.w >> 16) & 0xff);
+        }
+        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        const int len = dv.z & 0xffff;
+        const int l4o = dv.z >> 16;
+        const int ver = dv.w & 0xff;
+        const int proto = (dv.w >> 8) & 0xff;
+
+        bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
+        const bool raw = (fl & VPCSUM_F_RAW) != 0;
+        bool do_ip = false, do_l4 = false;
+        int fld = -1;
+        if (!bad && !raw) {
+            if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
+            else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
+            else bad = true;
+            if (!bad && (fl & VPCSUM_F_L4)) {
+                fld = l4_field(proto);
+                if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
+                else do_l4 = true;
+            }
+            if (!bad && (fl & VPCSUM_F_IP)) {
+                if (ver != 4) bad = true;
+                else do_ip = true;
+            }
+        }
+        const bool act = live && !bad;
+
+        // ---- per-packet plan (relative to the 16-B aligned base of the L3 header) ----
+        const uintptr_t l3a = (uintptr_t)(arena + off);
+        const uintptr_t basea = l3a & ~(uintptr_t)15;
+        PktPlan pl;
+        pl.r0 = (int)(l3a & 15);
+        const int need = !act ? 0 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
+        pl.nch = act ? (pl.r0 + need + 15) >> 4 : 0;
+        int fast_lo;
+        if (raw) {
+            pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
+            fast_lo = (pl.r0 + 15) & ~15;
+        } else if (do_l4) {
+            pl.l4lo = pl.r0 + l4o; pl.l4hi = pl.r0 + len; pl.fa = pl.r0 + l4o + fld;
+            fast_lo = (pl.fa + 2 + 15) & ~15;
+        } else {
+            pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
+            fast_lo = 1 << 30;
+        }
+        const int end_rel = pl.r0 + need;
+        const int H = min(fast_lo >> 4, pl.nch);   // header chunks [0, H), payload [H, nch)
+        if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
+        if (do_l4 && proto != 1) {
+            pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
+            pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
+        } else { pl.pslo = 0; pl.pshi = 0; }
+
+        // ---- header phase: one lane per packet, byte-masked ----
+        uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
+        uint32_t st_ip = 0, st_l4 = 0;
+        int hmax = H;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) hmax = max(hmax, __shfl_xor(hmax, m, 64));
+        const uint4* base = (const uint4*)basea;
+        for (int h = 0; h < hmax; h += UH) {
+            uint4 v[UH];
+#pragma unroll
+            for (int u = 0; u < UH; ++u) {
+                if (h + u < H) v[u] = ld_stream<NT>(base + h + u);
+                else v[u] = make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < UH; ++u) {
+                if (h + u >= H) continue;
+                const int c = (h + u) << 4;
+                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int d = c + 4 * j;
+                    const uint32_t mf = bmask(d, pl.fa, pl.fa + 2);
+                    acc_l4 += w[j] & bmask(d, pl.l4lo, pl.l4hi) & ~mf;
+                    const uint32_t mif = bmask(d, pl.r0 + 10, pl.r0 + 12);
+                    acc_ip += w[j] & bmask(d, pl.iplo, pl.iphi) & ~mif;
+                    acc_ps += w[j] & bmask(d, pl.pslo, pl.pshi);
+                    if (VERIFY) {
+                        st_l4 += w[j] & mf;
+                        st_ip += (w[j] & mif) & (do_ip ? 0xffffffffu : 0u);
+                    }
+                }
+            }
+        }
+
+        // ---- payload phase: TEAM lanes per packet, PPS packets at a time ----
+        const uint32_t blo = (uint32_t)basea, bhi = (uint32_t)((uint64_t)basea >> 32);
+        const int fast_hi = end_rel & ~15;
+        uint32_t my_payload = 0;
+#pragma unroll 1
+        for (int sidx = 0; sidx < TEAM; ++sidx) {
+            const int q = sidx * PPS + tid;
+            const uint32_t qlo = __shfl(blo, q, 64), qhi = __shfl(bhi, q, 64);
+            const int qH = __shfl(H, q, 64), qN = __shfl(pl.nch, q, 64);
+            const int qFH = __shfl(fast_hi, q, 64), qE = __shfl(end_rel, q, 64);
+            const uint4* qb = (const uint4*)(((uint64_t)qhi << 32) | qlo);
+            uint64_t acc = 0;
+            for (int r = 0; qH + r * TEAM < qN; r += U) {
+                uint4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int k = min(qH + (r + u) * TEAM + tl, qN - 1);
+                    v[u] = ld_stream<NT>(qb + k);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int k = qH + (r + u) * TEAM + tl;
+                    if (k >= qN) continue;
+                    const int c = k << 4;
+                    if (c + 16 <= qFH) {
+                        acc += (uint64_t)v[u].x + v[u].y;
+                        acc += (uint64_t)v[u].z + v[u].w;
+                    } else {
+                        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc += w[j] & tailmask(c + 4 * j, qE);
+                    }
+                }
+            }
+            const uint32_t ssum = team_sum<TEAM>(fold64(acc));
+            const uint32_t got = __shfl(ssum, (lane % PPS) * TEAM, 64);
+            if (lane / PPS == sidx) my_payload = got;
+        }
+
+        // ---- per-packet result (lane-parallel, coalesced stores) ----
+        if (!live) continue;
+        if (bad) {
+            if (out) out[p] = 0;
+            if (status) status[p] = VPCSUM_S_BAD_DESC;
+            continue;
+        }
+        uint32_t ipc = 0, l4c = 0;
+        uint8_t st = VPCSUM_S_DONE;
+        const uint32_t s_l4 = fold32(fold64(acc_l4) + my_payload);
+        if (raw) {
+            ipc = 0xffff - orient(s_l4, pl.r0);
+        } else {
+            if (do_ip) ipc = 0xffff - orient(fold64(acc_ip), pl.r0);
+            if (do_l4) {
+                uint32_t tot = orient(s_l4, pl.r0 + l4o);
+                if (proto != 1) {
+                    const uint32_t l4len = (uint32_t)(len - l4o);
+                    tot += orient(fold64(acc_ps), pl.r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
+                }
+                l4c = 0xffff - fold32(tot);
+                if (proto == 17 && l4c == 0) l4c = 0xffff;
+            }
+            if (VERIFY) {
+                if (do_ip && orient(fold32(st_ip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
+                if (do_l4) {
+                    const uint32_t stored = orient(fold32(st_l4), pl.fa);
+                    if (stored == l4c) st |= VPCSUM_S_L4_OK;
+                    if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                }
+            }
+            if (arena_w) {
+                uint8_t* w = arena_w + off;
+                if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
+                if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
+            }
+        }
+        if (out) out[p] = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
+        if (status) status[p] = st;
+    }
+}
+
+template <int TEAM, int U, int UH>
+static hipError_t launch_wave(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
+                              uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
+                              uint8_t* arena_w, int grid, hipStream_t stream) {
+    uint32_t need = (n + 255) / 256;   // 4 waves x 64 packets per workgroup
+    uint32_t g = grid > 0 ? (uint32_t)grid : need;
+    if (g > need) g = need;
+    if (g == 0) g = 1;
+#define VPC_LAUNCH(V, N)                                                                                         \
+    hipLaunchKernelGGL((k_csum_wave<TEAM, U, UH, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,          \
+                       (const uint4*)desc, n, out, status, flags_override, arena_w)
+    if (verify) {
+        if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
+    } else {
+        if (nt) VPC_LAUNCH(false, true); else VPC_LAUNCH(false, false);
+    }
+#undef VPC_LAUNCH
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// K1c: header-spread form.  One team of TEAM lanes per packet; the first 64 bytes from the
+// 16-B aligned L3 base (IPv4 header + pseudo addresses + L4 header + checksum field for every
+// ihl<=5+TCP / UDP / ICMP / IPv6-without-options packet) are split into 16/TEAM dwords per
+// lane, so the byte-masked work is 1-4 dwords per lane instead of whole chunks on a few lanes.
+// Chunks from byte 64 on are payload (8-op fast path, one masked tail); the rare headers that
+// reach past byte 64 (IPv4 options, IPv6 extension headers) take the generic masked path there.
+// All U payload loads of a lane are issued before the first is consumed.
+// ------------------------------------------------------------------------------------------
+// Header loads use the same (non-temporal) policy as the payload loads of the same 128-B line:
+// mixing a temporal and a non-temporal load on one line fetched it twice (FETCH_SIZE +30%).
+template <int HDW>
+struct HdrLoad;
+template <> struct HdrLoad<1> { typedef uint32_t T; };
+template <> struct HdrLoad<2> { typedef unsigned int T __attribute__((ext_vector_type(2))); };
+template <> struct HdrLoad<4> { typedef unsigned int T __attribute__((ext_vector_type(4))); };
+template <int HDW, bool NT>
+__device__ __forceinline__ typename HdrLoad<HDW>::T ld_hdr(uintptr_t a) {
+    typedef __attribute__((address_space(1))) const typename HdrLoad<HDW>::T GT;
+    return NT ? __builtin_nontemporal_load((GT*)a) : *(GT*)a;
+}
+
+__device__ __forceinline__ void hdr_dword(uint32_t w, int d, const PktPlan& pl, bool do_ip, uint64_t& acc_l4,
+                                          uint64_t& acc_ip, uint64_t& acc_ps, uint32_t& st_l4, uint32_t& st_ip,
+                                          bool verify) {
+    const uint32_t mf = bmask(d, pl.fa, pl.fa + 2);
+    acc_l4 += w & bmask(d, pl.l4lo, pl.l4hi) & ~mf;
+    const uint32_t mif = bmask(d, pl.r0 + 10, pl.r0 + 12);
+    acc_ip += w & bmask(d, pl.iplo, pl.iphi) & ~mif;
+    acc_ps += w & bmask(d, pl.pslo, pl.pshi);
+    if (verify) {
+        st_l4 += w & mf;
+        st_ip += (w & mif) & (do_ip ? 0xffffffffu : 0u);
+    }
+}
+
+__device__ __noinline__ void hdr_chunk_cold(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int c,
+                                            const PktPlan& pl, bool do_ip, uint64_t& acc_l4, uint64_t& acc_ip,
+                                            uint64_t& acc_ps, uint32_t& st_l4, uint32_t& st_ip, bool verify) {
+    hdr_dword(w0, c, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, verify);
+    hdr_dword(w1, c + 4, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, verify);
+    hdr_dword(w2, c + 8, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, verify);
+    hdr_dword(w3, c + 12, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, verify);
+}
+
+template <int TEAM, int U, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) void k_csum3(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                               const uint4* __restrict__ desc, uint32_t n,
+                                               uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                               const uint8_t* __restrict__ flags_override,
+                                               uint8_t* __restrict__ arena_w) {
+    constexpr int HDW = 16 / TEAM;   // header dwords per lane (64 B per team)
+    typedef typename HdrLoad<HDW>::T HT;
+    const int tl = threadIdx.x & (TEAM - 1);
+    const uint32_t team = (blockIdx.x * 256u + threadIdx.x) / TEAM;
+    const uint32_t nteams = gridDim.x * (256u / TEAM);
+
+    uint4 dnext = make_uint4(0, 0, 0, 0);
+    int fnext = 0;
+    if (team < n) {
+        dnext = desc[team];
+        if (flags_override) fnext = flags_override[team];
+    }
+
+    for (uint32_t p = team; p < n; p += nteams) {
+        const uint4 dv = dnext;
+        const int fov = fnext;
+        if (p + nteams < n) {
+            dnext = desc[p + nteams];
+            if (flags_override) fnext = flags_override[p + nteams];
+        }
+        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        const int len = dv.z & 0xffff;
+        const int l4o = dv.z >> 16;
+        const int ver = dv.w & 0xff;
+        const int proto = (dv.w >> 8) & 0xff;
+        const int fl = flags_override ? fov : (int)((dv.w >> 16) & 0xff);
+
+        bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
+        const bool raw = (fl & VPCSUM_F_RAW) != 0;
+        bool do_ip = false, do_l4 = false;
+        int fld = -1;
+        if (!bad && !raw) {
+            if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
+            else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
+            else bad = true;
+            if (!bad && (fl & VPCSUM_F_L4)) {
+                fld = l4_field(proto);
+                if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
+                else do_l4 = true;
+            }
+            if (!bad && (fl & VPCSUM_F_IP)) {
+                if (ver != 4) bad = true;
+                else do_ip = true;
+            }
+        }
+        if (bad) {
+            if (tl == 0) {
+                if (out) out[p] = 0;
+                if (status) status[p] = VPCSUM_S_BAD_DESC;
+            }
+            continue;
+        }
+
+        const uint8_t* l3 = arena + off;
+        const uintptr_t basea = (uintptr_t)l3 & ~(uintptr_t)15;
+        PktPlan pl;
+        pl.r0 = (int)((uintptr_t)l3 & 15);
+        const int need = (raw || do_l4) ? len : (do_ip ? l4o : 0);
+        const int end_rel = pl.r0 + need;
+        pl.nch = (end_rel + 15) >> 4;
+        if (raw) {
+            pl.l4lo = pl.r0; pl.l4hi = end_rel; pl.fa = -64;
+            pl.fast_lo = 0;
+        } else if (do_l4) {
+            pl.l4lo = pl.r0 + l4o; pl.l4hi = end_rel; pl.fa = pl.r0 + l4o + fld;
+            pl.fast_lo = (pl.fa + 2 + 15) & ~15;
+        } else {
+            pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
+            pl.fast_lo = 1 << 30;
+        }
+        pl.fast_hi = end_rel & ~15;
+        if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
+        if (do_l4 && proto != 1) {
+            pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
+            pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
+        } else { pl.pslo = 0; pl.pshi = 0; }
+
+        uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
+        uint32_t st_ip = 0, st_l4 = 0;
+        if (end_rel > 0) {
+            // ---- issue: header dwords (64 B per team) + all payload chunks of this group ----
+            const int d0 = tl * HDW * 4;                    // first header byte of this lane
+            const int dlast = (end_rel - 1) & ~(HDW * 4 - 1);   // last in-range load of this width
+            const HT hv = ld_hdr<HDW, NT>(basea + min(d0, dlast));
+            const uint4* base = (const uint4*)basea;
+            const int npay = pl.nch - 4;                    // payload chunks [4, nch)
+            for (int r = 0; r == 0 || r * TEAM < npay; r += U) {
+                uint4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int k = 4 + min((r + u) * TEAM + tl, npay - 1);
+                    if (npay > 0) v[u] = ld_stream<NT>(base + k);
+                    else v[u] = make_uint4(0, 0, 0, 0);
+                }
+                if (r == 0) {
+                    const uint32_t* hw = (const uint32_t*)&hv;
+#pragma unroll
+                    for (int j = 0; j < HDW; ++j)
+                        hdr_dword(hw[j], d0 + 4 * j, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int kk = (r + u) * TEAM + tl;
+                    if (kk >= npay) continue;
+                    const int c = (4 + kk) << 4;
+                    if (c >= pl.fast_lo && c + 16 <= pl.fast_hi) {
+                        acc_l4 += (uint64_t)v[u].x + v[u].y;
+                        acc_l4 += (uint64_t)v[u].z + v[u].w;
+                    } else if (c >= pl.fast_lo) {
+                        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
+                    } else {
+                        // long header (IPv4 options / IPv6 ext headers / IP-only): generic masks
+                        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            hdr_dword(w[j], c + 4 * j, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
+                    }
+                }
+            }
+        }
+
+        const uint32_t s_l4 = team_sum<TEAM>(fold64(acc_l4));
+        const uint32_t s_ip = team_sum<TEAM>(fold64(acc_ip));
+        const uint32_t s_ps = team_sum<TEAM>(fold64(acc_ps));
+        uint32_t s_stl4 = 0, s_stip = 0;
+        if (VERIFY) {
+            s_stl4 = team_sum<TEAM>(fold32(st_l4));
+            s_stip = team_sum<TEAM>(fold32(st_ip));
+        }
+        if (tl == 0) {
+            uint32_t ipc = 0, l4c = 0;
+            uint8_t st = VPCSUM_S_DONE;
+            if (raw) {
+                ipc = 0xffff - orient(fold32(s_l4), pl.r0);
+            } else {
+                if (do_ip) ipc = 0xffff - orient(fold32(s_ip), pl.r0);
+                if (do_l4) {
+                    uint32_t tot = orient(fold32(s_l4), pl.r0 + l4o);
+                    if (proto != 1) {
+                        const uint32_t l4len = (uint32_t)(len - l4o);
+                        tot += orient(fold32(s_ps), pl.r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
+                    }
+                    l4c = 0xffff - fold32(tot);
+                    if (proto == 17 && l4c == 0) l4c = 0xffff;
+                }
+                if (VERIFY) {
+                    if (do_ip && orient(fold32(s_stip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
+                    if (do_l4) {
+                        const uint32_t stored = orient(fold32(s_stl4), pl.fa);
+                        if (stored == l4c) st |= VPCSUM_S_L4_OK;
+                        if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                    }
+                }
+                if (arena_w) {
+                    uint8_t* w = arena_w + off;
+                    if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
+                    if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
+                }
+            }
+            if (out) out[p] = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
+            if (status) status[p] = st;
+        }
+    }
+}
+
+template <int TEAM, int U>
+static hipError_t launch_k3(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
+                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
+                            uint8_t* arena_w, int grid, hipStream_t stream) {
+    const uint32_t per_block = 256 / TEAM;
+    uint32_t need = (n + per_block - 1) / per_block;
+    uint32_t g = grid > 0 ? (uint32_t)grid : need;
+    if (g > need) g = need;
+    if (g == 0) g = 1;
+#define VPC_LAUNCH(V, N)                                                                                         \
+    hipLaunchKernelGGL((k_csum3<TEAM, U, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,                  \
+                       (const uint4*)desc, n, out, status, flags_override, arena_w)
+    if (verify) {
+        if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
+    } else {
+        if (nt) VPC_LAUNCH(false, true); else VPC_LAUNCH(false, false);
+    }
+#undef VPC_LAUNCH
+    return hipGetLastError();
+}
+
 template <int TEAM, int U>
 static hipError_t launch_team(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
-                              uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify,
+                              uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                               uint8_t* arena_w, int grid, hipStream_t stream) {
     const uint32_t per_block = 256 / TEAM;
     uint32_t need = (n + per_block - 1) / per_block;
     uint32_t g = grid > 0 ? (uint32_t)grid : need;
     if (g > need) g = need;
     if (g == 0) g = 1;
-    if (verify)
-        hipLaunchKernelGGL((k_csum<TEAM, U, true>), dim3(g), dim3(256), 0, stream, arena, arena_len,
-                           (const uint4*)desc, n, out, status, flags_override, arena_w);
-    else
-        hipLaunchKernelGGL((k_csum<TEAM, U, false>), dim3(g), dim3(256), 0, stream, arena, arena_len,
-                           (const uint4*)desc, n, out, status, flags_override, arena_w);
+#define VPC_LAUNCH(V, N)                                                                                         \
+    hipLaunchKernelGGL((k_csum<TEAM, U, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,                   \
+                       (const uint4*)desc, n, out, status, flags_override, arena_w)
+    if (verify) {
+        if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
+    } else {
+        if (nt) VPC_LAUNCH(false, true); else VPC_LAUNCH(false, false);
+    }
+#undef VPC_LAUNCH
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// K1 (buffer form, the default).  Same work split as k_csum, but the packet bytes come in
+// through buffer_load_dwordx4 on ONE wave-uniform descriptor spanning the arena: a chunk past
+// the packet end gets an offset outside the descriptor's range and the hardware returns zeros
+// without touching memory.  So all U loads of a lane are issued unconditionally (no branch,
+// nothing for the compiler to sink), address math is one 32-bit add per load, and the
+// per-chunk classification is a single range test.  Needs a 16-B aligned arena < 4 GiB;
+// launch_csum falls back to k_csum otherwise.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kOutOfRange = 0xFFFFFF00u;
+constexpr uint64_t kMaxBufArena = 0xFFFF0000ull;
+// The range check zeroes any dword that reaches past num_records, so the descriptor covers the
+// arena rounded up to 16 B: the 16-B aligned block holding the last arena byte is readable
+// (it never crosses a page), and bytes past the arena end are masked by the packet bounds.
+__device__ __forceinline__ uint32_t buf_records(uint64_t arena_len) {
+    return (uint32_t)((arena_len + 15) & ~15ull);
+}
+
+template <int TEAM, int U, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) void k_csum_b(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                const uint4* __restrict__ desc, uint32_t n,
+                                                uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                                const uint8_t* __restrict__ flags_override,
+                                                uint8_t* __restrict__ arena_w) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
+    const int tl = threadIdx.x & (TEAM - 1);
+    const uint32_t team = (blockIdx.x * 256u + threadIdx.x) / TEAM;
+    const uint32_t nteams = gridDim.x * (256u / TEAM);
+
+    uint4 dnext = make_uint4(0, 0, 0, 0);
+    int fnext = 0;
+    if (team < n) {
+        dnext = desc[team];
+        if (flags_override) fnext = flags_override[team];
+    }
+
+    for (uint32_t p = team; p < n; p += nteams) {
+        const uint4 dv = dnext;
+        const int fov = fnext;
+        if (p + nteams < n) {   // prefetch the next descriptor while this packet streams
+            dnext = desc[p + nteams];
+            if (flags_override) fnext = flags_override[p + nteams];
+        }
+        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        const int len = dv.z & 0xffff;
+        const int l4o = dv.z >> 16;
+        const int ver = dv.w & 0xff;
+        const int proto = (dv.w >> 8) & 0xff;
+        const int fl = flags_override ? fov : (int)((dv.w >> 16) & 0xff);
+
+        bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
+        const bool raw = (fl & VPCSUM_F_RAW) != 0;
+        bool do_ip = false, do_l4 = false;
+        int fld = -1;
+        if (!bad && !raw) {
+            if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
+            else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
+            else bad = true;
+            if (!bad && (fl & VPCSUM_F_L4)) {
+                fld = l4_field(proto);
+                if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
+                else do_l4 = true;
+            }
+            if (!bad && (fl & VPCSUM_F_IP)) {
+                if (ver != 4) bad = true;
+                else do_ip = true;
+            }
+        }
+        if (bad) {
+            if (tl == 0) {
+                if (out) out[p] = 0;
+                if (status) status[p] = VPCSUM_S_BAD_DESC;
+            }
+            continue;
+        }
+
+        PktPlan pl;
+        pl.r0 = (int)(off & 15);                          // arena is 16-B aligned
+        const uint32_t boff = (uint32_t)(off & ~(uint64_t)15);
+        const int need = (raw || do_l4) ? len : (do_ip ? l4o : 0);
+        pl.nch = (pl.r0 + need + 15) >> 4;
+        if (raw) {
+            pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
+            pl.fast_lo = (pl.r0 + 15) & ~15;
+        } else if (do_l4) {
+            pl.l4lo = pl.r0 + l4o; pl.l4hi = pl.r0 + len; pl.fa = pl.r0 + l4o + fld;
+            pl.fast_lo = (pl.fa + 2 + 15) & ~15;
+        } else {
+            pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
+            pl.fast_lo = 1 << 30;
+        }
+        pl.fast_hi = (pl.r0 + need) & ~15;
+        if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
+        if (do_l4 && proto != 1) {
+            pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
+            pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
+        } else { pl.pslo = 0; pl.pshi = 0; }
+        // chunk classes: k < klo header, klo <= k < khi payload, k >= khi tail (or past the end)
+        const int klo = min(pl.fast_lo >> 4, pl.nch);
+        const uint32_t kfast = (uint32_t)max((pl.fast_hi >> 4) - klo, 0);
+
+        uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
+        uint32_t st_ip = 0, st_l4 = 0;
+
+        for (int r0 = 0; r0 * TEAM < pl.nch; r0 += U) {
+            v4u v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = (r0 + u) * TEAM + tl;
+                const uint32_t bo = k < pl.nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = (r0 + u) * TEAM + tl;
+                if ((uint32_t)(k - klo) < kfast) {
+                    acc_l4 += (uint64_t)v[u].x + v[u].y;
+                    acc_l4 += (uint64_t)v[u].z + v[u].w;
+                } else if (k >= klo) {
+                    const int c = k << 4;
+                    const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
+                } else {
+                    const int c = k << 4;
+                    const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int d = c + 4 * j;
+                        const uint32_t mf = bmask(d, pl.fa, pl.fa + 2);
+                        acc_l4 += w[j] & bmask(d, pl.l4lo, pl.l4hi) & ~mf;
+                        const uint32_t mif = bmask(d, pl.r0 + 10, pl.r0 + 12);
+                        acc_ip += w[j] & bmask(d, pl.iplo, pl.iphi) & ~mif;
+                        acc_ps += w[j] & bmask(d, pl.pslo, pl.pshi);
+                        if (VERIFY) {
+                            st_l4 += w[j] & mf;
+                            st_ip += (w[j] & mif) & (do_ip ? 0xffffffffu : 0u);
+                        }
+                    }
+                }
+            }
+        }
+
+        const uint32_t s_l4 = team_sum<TEAM>(fold64(acc_l4));
+        const uint32_t s_ip = team_sum<TEAM>(fold64(acc_ip));
+        const uint32_t s_ps = team_sum<TEAM>(fold64(acc_ps));
+        uint32_t s_stl4 = 0, s_stip = 0;
+        if (VERIFY) {
+            s_stl4 = team_sum<TEAM>(fold32(st_l4));
+            s_stip = team_sum<TEAM>(fold32(st_ip));
+        }
+        if (tl == 0) {
+            uint32_t ipc = 0, l4c = 0;
+            uint8_t st = VPCSUM_S_DONE;
+            if (raw) {
+                ipc = 0xffff - orient(fold32(s_l4), pl.r0);
+            } else {
+                if (do_ip) ipc = 0xffff - orient(fold32(s_ip), pl.r0);
+                if (do_l4) {
+                    uint32_t tot = orient(fold32(s_l4), pl.r0 + l4o);
+                    if (proto != 1) {
+                        const uint32_t l4len = (uint32_t)(len - l4o);
+                        tot += orient(fold32(s_ps), pl.r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
+                    }
+                    l4c = 0xffff - fold32(tot);
+                    if (proto == 17 && l4c == 0) l4c = 0xffff;
+                }
+                if (VERIFY) {
+                    if (do_ip && orient(fold32(s_stip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
+                    if (do_l4) {
+                        const uint32_t stored = orient(fold32(s_stl4), pl.fa);
+                        if (stored == l4c) st |= VPCSUM_S_L4_OK;
+                        if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                    }
+                }
+                if (arena_w) {
+                    uint8_t* w = arena_w + off;
+                    if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
+                    if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
+                }
+            }
+            if (out) out[p] = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
+            if (status) status[p] = st;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// K1 (buffer form with coalesced results).  As k_csum_b, but a wave owns 64 consecutive
+// packets per super-iteration (TEAM iterations of 64/TEAM packets); each team's result is
+// shuffled to lane (packet - P0) and out/status are written with one 256-B / 64-B store per
+// 64 packets instead of one 4-B / 1-B store per team (the scattered stores cost 3-4% each).
+// ------------------------------------------------------------------------------------------
+template <int TEAM, int U, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                const uint4* __restrict__ desc, uint32_t n,
+                                                uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                                const uint8_t* __restrict__ flags_override,
+                                                uint8_t* __restrict__ arena_w) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    constexpr int PPI = 64 / TEAM;   // packets per iteration per wave
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
+    const int lane = threadIdx.x & 63;
+    const int tl = lane & (TEAM - 1);
+    const int tid = lane / TEAM;
+    const uint32_t gw = (blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t wstride = gridDim.x * 4u * 64u;
+
+    uint32_t P0 = gw * 64u;
+    uint4 dnext = make_uint4(0, 0, 0, 0);
+    int fnext = 0;
+    {
+        const uint32_t q = P0 + tid;
+        if (q < n) {
+            dnext = desc[q];
+            if (flags_override) fnext = flags_override[q];
+        }
+    }
+    for (; P0 < n; P0 += wstride) {
+        uint32_t res_out = 0, res_st = 0;
+#pragma unroll 1
+        for (int it = 0; it < TEAM; ++it) {
+            const uint32_t p = P0 + it * PPI + tid;
+            const uint4 dv = dnext;
+            const int fov = fnext;
+            {   // prefetch the descriptor of this team's next packet
+                const uint32_t q = (it + 1 < TEAM) ? p + PPI : P0 + wstride + tid;
+                if (q < n) {
+                    dnext = desc[q];
+                    if (flags_override) fnext = flags_override[q];
+                }
+            }
+            const bool live = p < n;
+            const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+            const int len = dv.z & 0xffff;
+            const int l4o = dv.z >> 16;
+            const int ver = dv.w & 0xff;
+            const int proto = (dv.w >> 8) & 0xff;
+            const int fl = flags_override ? fov : (int)((dv.w >> 16) & 0xff);
+
+            bool bad = !live || off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
+            const bool raw = (fl & VPCSUM_F_RAW) != 0;
+            bool do_ip = false, do_l4 = false;
+            int fld = -1;
+            if (!bad && !raw) {
+                if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
+                else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
+                else bad = true;
+                if (!bad && (fl & VPCSUM_F_L4)) {
+                    fld = l4_field(proto);
+                    if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
+                    else do_l4 = true;
+                }
+                if (!bad && (fl & VPCSUM_F_IP)) {
+                    if (ver != 4) bad = true;
+                    else do_ip = true;
+                }
+            }
+
+            PktPlan pl;
+            pl.r0 = (int)(off & 15);
+            const uint32_t boff = (uint32_t)(off & ~(uint64_t)15);
+            const int need = bad ? 0 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
+            pl.nch = bad ? 0 : (pl.r0 + need + 15) >> 4;
+            if (raw) {
+                pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
+                pl.fast_lo = (pl.r0 + 15) & ~15;
+            } else if (do_l4) {
+                pl.l4lo = pl.r0 + l4o; pl.l4hi = pl.r0 + len; pl.fa = pl.r0 + l4o + fld;
+                pl.fast_lo = (pl.fa + 2 + 15) & ~15;
+            } else {
+                pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
+                pl.fast_lo = 1 << 30;
+            }
+            pl.fast_hi = (pl.r0 + need) & ~15;
+            if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
+            if (do_l4 && proto != 1) {
+                pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
+                pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
+            } else { pl.pslo = 0; pl.pshi = 0; }
+            const int klo = min(pl.fast_lo >> 4, pl.nch);
+            const uint32_t kfast = (uint32_t)max((pl.fast_hi >> 4) - klo, 0);
+
+            uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
+            uint32_t st_ip = 0, st_l4 = 0;
+            for (int r0 = 0; r0 * TEAM < pl.nch; r0 += U) {
+                v4u v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int k = (r0 + u) * TEAM + tl;
+                    const uint32_t bo = k < pl.nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
+                    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+                }
+                // payload chunks first; the byte-masked header chunk (u == 0 of the first group)
+                // last, when the other U-1 data registers are already dead
+#pragma unroll
+                for (int u = 1; u <= U; ++u) {
+                    const int uu = u % U;
+                    const int k = (r0 + uu) * TEAM + tl;
+                    if ((uint32_t)(k - klo) < kfast) {
+                        acc_l4 += (uint64_t)v[uu].x + v[uu].y;
+                        acc_l4 += (uint64_t)v[uu].z + v[uu].w;
+                    } else if (k >= klo) {
+                        const int c = k << 4;
+                        const uint32_t w[4] = {v[uu].x, v[uu].y, v[uu].z, v[uu].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
+                    } else {
+                        // header chunk (u > 0 only for headers longer than TEAM chunks)
+                        const int c = k << 4;
+                        const uint32_t w[4] = {v[uu].x, v[uu].y, v[uu].z, v[uu].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            hdr_dword(w[j], c + 4 * j, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
+                    }
+                }
+            }
+
+            const uint32_t s_l4 = team_sum<TEAM>(fold64(acc_l4));
+            const uint32_t s_ip = team_sum<TEAM>(fold64(acc_ip));
+            const uint32_t s_ps = team_sum<TEAM>(fold64(acc_ps));
+            uint32_t s_stl4 = 0, s_stip = 0;
+            if (VERIFY) {
+                s_stl4 = team_sum<TEAM>(fold32(st_l4));
+                s_stip = team_sum<TEAM>(fold32(st_ip));
+            }
+            uint32_t ro = 0, rs = VPCSUM_S_BAD_DESC;
+            if (!bad) {
+                uint32_t ipc = 0, l4c = 0;
+                uint32_t st = VPCSUM_S_DONE;
+                if (raw) {
+                    ipc = 0xffff - orient(fold32(s_l4), pl.r0);
+                } else {
+                    if (do_ip) ipc = 0xffff - orient(fold32(s_ip), pl.r0);
+                    if (do_l4) {
+                        uint32_t tot = orient(fold32(s_l4), pl.r0 + l4o);
+                        if (proto != 1) {
+                            const uint32_t l4len = (uint32_t)(len - l4o);
+                            tot += orient(fold32(s_ps), pl.r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
+                        }
+                        l4c = 0xffff - fold32(tot);
+                        if (proto == 17 && l4c == 0) l4c = 0xffff;
+                    }
+                    if (VERIFY) {
+                        if (do_ip && orient(fold32(s_stip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
+                        if (do_l4) {
+                            const uint32_t stored = orient(fold32(s_stl4), pl.fa);
+                            if (stored == l4c) st |= VPCSUM_S_L4_OK;
+                            if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                        }
+                    }
+                    if (arena_w && tl == 0) {
+                        uint8_t* w = arena_w + off;
+                        if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
+                        if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
+                    }
+                }
+                ro = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
+                rs = st;
+            }
+            // hand the team's result to the lane that owns packet P0 + lane
+            const int src = (lane % PPI) * TEAM;
+            const uint32_t go = __shfl(ro, src, 64);
+            const uint32_t gs = __shfl(rs, src, 64);
+            if (lane / PPI == it) { res_out = go; res_st = gs; }
+        }
+        if (P0 + lane < n) {
+            if (NT) {   // results are written once: stream them past the caches like the reads
+                if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lane));
+                if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lane));
+            } else {
+                if (out) out[P0 + lane] = res_out;
+                if (status) status[P0 + lane] = (uint8_t)res_st;
+            }
+        }
+    }
+}
+
+template <int TEAM, int U>
+static hipError_t launch_c(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
+                           uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
+                           uint8_t* arena_w, int grid, hipStream_t stream) {
+    if (arena_len > kMaxBufArena || ((uintptr_t)arena & 15))
+        return launch_team<TEAM, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w,
+                                    grid, stream);
+    uint32_t need = (n + 255) / 256;   // 4 waves x 64 packets per workgroup
+    uint32_t g = grid > 0 ? (uint32_t)grid : need;
+    if (g > need) g = need;
+    if (g == 0) g = 1;
+#define VPC_LAUNCH(V, N)                                                                                         \
+    hipLaunchKernelGGL((k_csum_c<TEAM, U, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
+                       (const uint4*)desc, n, out, status, flags_override, arena_w)
+    if (verify) {
+        if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
+    } else {
+        if (nt) VPC_LAUNCH(false, true); else VPC_LAUNCH(false, false);
+    }
+#undef VPC_LAUNCH
+    return hipGetLastError();
+}
+
+template <int TEAM, int U>
+static hipError_t launch_b(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
+                           uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
+                           uint8_t* arena_w, int grid, hipStream_t stream) {
+    if (arena_len > kMaxBufArena || ((uintptr_t)arena & 15))   // descriptor range / alignment
+        return launch_team<TEAM, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w,
+                                    grid, stream);
+    const uint32_t per_block = 256 / TEAM;
+    uint32_t need = (n + per_block - 1) / per_block;
+    uint32_t g = grid > 0 ? (uint32_t)grid : need;
+    if (g > need) g = need;
+    if (g == 0) g = 1;
+#define VPC_LAUNCH(V, N)                                                                                         \
+    hipLaunchKernelGGL((k_csum_b<TEAM, U, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
+                       (const uint4*)desc, n, out, status, flags_override, arena_w)
+    if (verify) {
+        if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
+    } else {
+        if (nt) VPC_LAUNCH(false, true); else VPC_LAUNCH(false, false);
+    }
+#undef VPC_LAUNCH
     return hipGetLastError();
 }
 
@@ -276,14 +1208,42 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         (void)hipGetDevice(&dev);
         grid = num_cus(dev) * 8;   // 8 blocks x 4 waves = 32 waves per CU
     }
+    // mode bit 13 (internal tuning): plain loads instead of non-temporal ones
+    const bool nt = (mode & 0x2000u) == 0;
+    // variant = (lanes per packet, chunks in flight per lane); ids 2..6 are log2(lanes)
+#define VPC_T(T, U) launch_team<T, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream)
     switch (team_log2) {
-        case 2: return launch_team<4, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, arena_w, grid, stream);
-        case 3: return launch_team<8, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, arena_w, grid, stream);
-        case 5: return launch_team<32, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, arena_w, grid, stream);
-        case 6: return launch_team<64, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, arena_w, grid, stream);
-        case 4:
-        default: return launch_team<16, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, arena_w, grid, stream);
+        case 2: return VPC_T(4, 4);
+        case 3: return VPC_T(8, 4);
+        case 4: return VPC_T(16, 8);
+        case 5: return VPC_T(32, 4);
+        case 6: return VPC_T(64, 4);
+        case 7: return VPC_T(4, 8);
+        case 8: return VPC_T(8, 6);
+        case 9: return VPC_T(8, 12);
+        case 10: return VPC_T(16, 4);
+        case 11: return VPC_T(8, 8);
+        case 12: return launch_wave<8, 4, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 13: return launch_wave<8, 8, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 14: return launch_wave<16, 4, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 15: return launch_wave<4, 8, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 16: return launch_k3<8, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 17: return launch_k3<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 18: return launch_k3<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 19: return launch_k3<16, 3>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 20: return launch_k3<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 21: return launch_b<8, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 22: return launch_b<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 23: return launch_b<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 24: return launch_b<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 25: return launch_b<16, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 26: return launch_c<8, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 27: return launch_c<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 28: return launch_c<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 29: return launch_c<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        default: return launch_c<kDefaultTeam, kDefaultUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
     }
+#undef VPC_T
 }
 
 // ------------------------------------------------------------------------------------------
