@@ -1,0 +1,88 @@
+"""Host-memory (PCIe-inclusive) rate of the checksum path, for DESIGN.md (tooling).
+
+The vswitch path starts and ends in host memory (tap/tun buffers, AF_XDP umem).  Measured:
+  * pipeline: page-locked host arena of C2 frames -> chunked H2D (2-D copy of the 1504 B each
+    frame needs) || kernel || D2H of 4-B results, two streams (vpcsum_ctx_pipeline);
+  * zero-copy: the kernel reads the page-locked host arena directly over PCIe;
+  * submit/wait latency of small batches (the per-completeTx flush of the Java integration).
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vproxy_amd import vpcsum as V  # noqa: E402
+from bench import algorithmic_bytes  # noqa: E402
+
+res = {}
+n, stride = 1 << 20, 2048
+# frames generated on the device, copied once into page-locked host memory
+d_arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+d_desc = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+V.synth(d_arena, n, stride, 0, V.SYNTH_C2, 0x20241020, 0, d_desc)
+torch.cuda.synchronize()
+h_arena = d_arena.cpu().pin_memory()
+h_desc_t = d_desc.cpu().pin_memory()
+desc = h_desc_t.numpy().view(V.DESC_DTYPE)
+nbytes = algorithmic_bytes(desc)
+ref = torch.zeros(n, dtype=torch.int32, device="cuda")
+V.compute(d_arena, d_desc, n, ref, None)
+torch.cuda.synchronize()
+ref_np = ref.cpu().numpy().view(np.uint32)
+del d_arena
+
+ctx = V.Context(0, max_arena=(n // 4) * stride + 4096, max_pkts=n // 4)
+arena_np = h_arena.numpy()
+out = torch.zeros(n, dtype=torch.int32).pin_memory().numpy().view(np.uint32)
+# torch pin_memory() buffers are hipHostMalloc'd: the context recognises them as page-locked
+
+pipe = {}
+for chunks in (4, 8, 16, 32):
+    out[:] = 0
+    ctx.pipeline(arena_np, stride, 1504, desc, out, chunks=chunks)   # warm
+    t = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        ctx.pipeline(arena_np, stride, 1504, desc, out, chunks=chunks)
+    dt = (time.perf_counter() - t) / reps
+    assert np.array_equal(out, ref_np)
+    pipe[chunks] = {"ms": round(dt * 1e3, 3), "GBps_algorithmic": round(nbytes / dt / 1e9, 2),
+                    "Mpps": round(n / dt / 1e6, 2)}
+res["pipeline_h2d_kernel_d2h"] = pipe
+
+# zero-copy: kernel reads the page-locked host arena in place (PCIe reads, no staging copy)
+zc_out = torch.zeros(n, dtype=torch.int32, device="cuda")
+h_desc_dev = h_desc_t.cuda()
+V.compute(h_arena, h_desc_dev, n, zc_out, None)
+torch.cuda.synchronize()
+t = time.perf_counter()
+for _ in range(3):
+    V.compute(h_arena, h_desc_dev, n, zc_out, None)
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t) / 3
+assert np.array_equal(zc_out.cpu().numpy().view(np.uint32), ref_np)
+res["zero_copy_kernel_reads_host"] = {"ms": round(dt * 1e3, 3), "GBps_algorithmic": round(nbytes / dt / 1e9, 2)}
+
+# small-batch submit/wait latency (per completeTx flush), pageable arena path
+lat = {}
+small_arena = arena_np[: 8192 * stride].copy()
+for b in (32, 128, 1024, 8192):
+    dsc = desc[:b].copy()
+    o = np.zeros(b, np.uint32)
+    for _ in range(5):
+        ctx.wait(ctx.submit(small_arena, dsc, o))
+    ts = []
+    for _ in range(50):
+        t = time.perf_counter()
+        ctx.wait(ctx.submit(small_arena, dsc, o))
+        ts.append(time.perf_counter() - t)
+    assert np.array_equal(o, ref_np[:b])
+    lat[b] = {"median_us": round(float(np.median(ts)) * 1e6, 1), "p99_us": round(float(np.percentile(ts, 99)) * 1e6, 1),
+              "Mpps": round(b / float(np.median(ts)) / 1e6, 3)}
+res["submit_wait_latency"] = lat
+res["config"] = "C2: 1,048,576 x 1500 B IPv4/TCP, stride 2048, 1504 B copied per frame"
+print(json.dumps(res))

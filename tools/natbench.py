@@ -1,0 +1,31 @@
+"""NAT / TTL rewrite throughput (BASELINE config C5 per GPU), RFC 1624 and strict-Java modes."""
+import json, os, sys, time
+import numpy as np, torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vproxy_amd import vpcsum as V  # noqa: E402
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000 // 8
+stride = 2048
+arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+V.synth(arena, n, stride, 0, V.SYNTH_C3, 0x20241020, 0, d)
+# C5: 1500 B TCP/UDP with valid checksums -> use C2 lengths but alternate TCP/UDP via the C3 mix
+V.compute(arena, d, n, None, None, V.MODE_WRITE)
+g = torch.Generator(device="cpu").manual_seed(5)
+rw = torch.randint(0, 256, (n, 16), dtype=torch.uint8, generator=g)
+rw[:, 12] = V.NAT_SRC | V.NAT_DST | V.NAT_SPORT | V.NAT_DPORT
+rw[:, 13:] = 0
+rw = rw.cuda()
+st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+res = {"packets": n}
+for name, mode in (("rfc1624", V.NAT_RFC1624), ("strict_java", V.NAT_STRICT_JAVA)):
+    for _ in range(3):
+        V.nat4(arena, d, rw, n, st, mode)
+    e0, e1 = V.Event(), V.Event()
+    e0.record()
+    it = 10
+    for _ in range(it):
+        V.nat4(arena, d, rw, n, st, mode)
+    e1.record()
+    ms = e0.elapsed_ms(e1) / it
+    res[name] = {"ms": round(ms, 4), "Mpps": round(n / ms / 1e3, 1), "GBps_at_72B": round(n * 72 / ms / 1e6, 1)}
+print(json.dumps(res))

@@ -296,6 +296,13 @@ int vpcsum_ctx_unregister_arena(vpcsum_ctx_t* c, void* h_arena) {
 static bool is_registered(vpcsum_ctx* c, const uint8_t* p, uint64_t len) {
     for (auto& r : c->registered)
         if (p >= r.first && p + len <= r.first + r.second) return true;
+    // page-locked elsewhere (hipHostMalloc, another library's hipHostRegister)?
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost) {
+        hipPointerAttribute_t b;
+        if (hipPointerGetAttributes(&b, p + len - 1) == hipSuccess && b.type == hipMemoryTypeHost) return true;
+    }
+    (void)hipGetLastError();
     return false;
 }
 

@@ -86,7 +86,7 @@ constexpr int kFlagRejected = 0x80;
 // result write) is issued once per wave for 64/TEAM packets, so small teams amortise it;
 // the payload loop costs the same per byte for any TEAM.
 constexpr int kDefaultTeam = 8;
-constexpr int kDefaultUnroll = 12;
+constexpr int kDefaultUnroll = 6;
 
 template <int TEAM>
 __device__ __forceinline__ uint32_t team_sum(uint32_t v) {
@@ -545,6 +545,16 @@ __device__ __forceinline__ void hdr_dword(uint32_t w, int d, const PktPlan& pl, 
     }
 }
 
+// [lo, hi) as a 32-bit halfword mask (bits clipped to 0..31)
+__device__ __forceinline__ uint32_t hw_range(int lo, int hi) {
+    const uint32_t mh = hi >= 32 ? 0xffffffffu : (hi <= 0 ? 0u : ((1u << hi) - 1u));
+    const uint32_t ml = lo >= 32 ? 0xffffffffu : (lo <= 0 ? 0u : ((1u << lo) - 1u));
+    return mh & ~ml;
+}
+__device__ __forceinline__ uint32_t hw_bit(int b) { return (b >= 0 && b < 32) ? (1u << b) : 0u; }
+// 2 halfword-select bits -> dword byte mask: bit0 -> 0x0000ffff, bit1 -> 0xffff0000
+__device__ __forceinline__ uint32_t hmask(uint32_t b) { return ((b & 1u) | ((b & 2u) << 15)) * 0xffffu; }
+
 __device__ __noinline__ void hdr_chunk_cold(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int c,
                                             const PktPlan& pl, bool do_ip, uint64_t& acc_l4, uint64_t& acc_ip,
                                             uint64_t& acc_ps, uint32_t& st_l4, uint32_t& st_ip, bool verify) {
@@ -964,7 +974,7 @@ __global__ __launch_bounds__(256) void k_csum_b(const uint8_t* __restrict__ aren
 // shuffled to lane (packet - P0) and out/status are written with one 256-B / 64-B store per
 // 64 packets instead of one 4-B / 1-B store per team (the scattered stores cost 3-4% each).
 // ------------------------------------------------------------------------------------------
-template <int TEAM, int U, bool VERIFY, bool NT>
+template <int TEAM, int U, bool VERIFY, bool NT, int ABL = 0>
 __global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -1054,35 +1064,83 @@ __global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ aren
             } else { pl.pslo = 0; pl.pshi = 0; }
             const int klo = min(pl.fast_lo >> 4, pl.nch);
             const uint32_t kfast = (uint32_t)max((pl.fast_hi >> 4) - klo, 0);
+            // Halfword bitmaps over the first 64 B from the aligned base (even L3 start, even L4
+            // offset, no odd end inside the window): bit h selects bytes [2h, 2h+2).  B_l4 also
+            // carries the pseudo-header addresses (same orientation when l4o is even), so the
+            // common header costs ~7 ops per dword and range instead of a byte-mask chain.
+            const bool hbm = !raw && !(pl.r0 & 1) && !(l4o & 1) && ((((pl.r0 + need) & 1) == 0) || pl.r0 + need >= 64);
+            uint32_t B_ip = 0, B_l4 = 0, F_ip = 0, F_l4 = 0;
+            if (hbm) {
+                const int r0h = pl.r0 >> 1;
+                if (do_ip) {
+                    F_ip = 1u << (r0h + 5);
+                    B_ip = hw_range(r0h, r0h + (l4o >> 1)) & ~F_ip;
+                }
+                if (do_l4) {
+                    F_l4 = hw_bit(pl.fa >> 1);
+                    B_l4 = hw_range((pl.r0 + l4o) >> 1, (pl.r0 + need + 1) >> 1) & ~F_l4;
+                    if (proto != 1) B_l4 |= (ver == 4) ? hw_range(r0h + 6, r0h + 10) : hw_range(r0h + 4, r0h + 20);
+                }
+            }
 
             uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
             uint32_t st_ip = 0, st_l4 = 0;
-            for (int r0 = 0; r0 * TEAM < pl.nch; r0 += U) {
-                v4u v[U];
+            // fast class: every header byte lies in the 64-B bitmap window.  The rare rest (odd
+            // alignment, IPv4 options / IPv6 extension headers past byte 64, raw ranges) takes a
+            // separate one-chunk-at-a-time loop, so its byte-mask temporaries never share
+            // registers with the U chunks in flight of the main loop.
+            const bool fastc = hbm && klo <= 4;
+            if (fastc) {
+                for (int r0 = 0; r0 * TEAM < pl.nch; r0 += U) {
+                    v4u v[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int k = (r0 + u) * TEAM + tl;
-                    const uint32_t bo = k < pl.nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
-                    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+                    for (int u = 0; u < U; ++u) {
+                        const int k = (r0 + u) * TEAM + tl;
+                        const uint32_t bo = k < pl.nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
+                        v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int k = (r0 + u) * TEAM + tl;
+                        if ((ABL & 1) || (uint32_t)(k - klo) < kfast) {   // ABL&1: ablation, no masks
+                            acc_l4 += (uint64_t)v[u].x + v[u].y;
+                            acc_l4 += (uint64_t)v[u].z + v[u].w;
+                        } else if (k >= klo) {
+                            const int c = k << 4;
+                            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
+                        } else if (u == 0) {
+                            // header chunk: k < klo <= 4 <= TEAM, so only u == 0 of the first group
+                            const int hb0 = k << 3;   // halfwords [8k, 8k+8)
+                            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const int hb = hb0 + 2 * j;
+                                acc_ip += w[j] & hmask((B_ip >> hb) & 3);
+                                acc_l4 += w[j] & hmask((B_l4 >> hb) & 3);
+                                if (VERIFY) {
+                                    st_ip += w[j] & hmask((F_ip >> hb) & 3);
+                                    st_l4 += w[j] & hmask((F_l4 >> hb) & 3);
+                                }
+                            }
+                        }
+                    }
                 }
-                // payload chunks first; the byte-masked header chunk (u == 0 of the first group)
-                // last, when the other U-1 data registers are already dead
-#pragma unroll
-                for (int u = 1; u <= U; ++u) {
-                    const int uu = u % U;
-                    const int k = (r0 + uu) * TEAM + tl;
+            } else {
+                for (int r = 0; r * TEAM < pl.nch; ++r) {
+                    const int k = r * TEAM + tl;
+                    const uint32_t bo = k < pl.nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
+                    const v4u vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+                    const int c = k << 4;
+                    const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
                     if ((uint32_t)(k - klo) < kfast) {
-                        acc_l4 += (uint64_t)v[uu].x + v[uu].y;
-                        acc_l4 += (uint64_t)v[uu].z + v[uu].w;
+                        acc_l4 += (uint64_t)w[0] + w[1];
+                        acc_l4 += (uint64_t)w[2] + w[3];
                     } else if (k >= klo) {
-                        const int c = k << 4;
-                        const uint32_t w[4] = {v[uu].x, v[uu].y, v[uu].z, v[uu].w};
 #pragma unroll
                         for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
                     } else {
-                        // header chunk (u > 0 only for headers longer than TEAM chunks)
-                        const int c = k << 4;
-                        const uint32_t w[4] = {v[uu].x, v[uu].y, v[uu].z, v[uu].w};
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
                             hdr_dword(w[j], c + 4 * j, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
@@ -1090,9 +1148,9 @@ __global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ aren
                 }
             }
 
-            const uint32_t s_l4 = team_sum<TEAM>(fold64(acc_l4));
-            const uint32_t s_ip = team_sum<TEAM>(fold64(acc_ip));
-            const uint32_t s_ps = team_sum<TEAM>(fold64(acc_ps));
+            const uint32_t s_l4 = (ABL & 2) ? fold64(acc_l4) : team_sum<TEAM>(fold64(acc_l4));
+            const uint32_t s_ip = (ABL & 2) ? fold64(acc_ip) : team_sum<TEAM>(fold64(acc_ip));
+            const uint32_t s_ps = (ABL & 2) ? fold64(acc_ps) : team_sum<TEAM>(fold64(acc_ps));
             uint32_t s_stl4 = 0, s_stip = 0;
             if (VERIFY) {
                 s_stl4 = team_sum<TEAM>(fold32(st_l4));
@@ -1150,7 +1208,7 @@ __global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ aren
     }
 }
 
-template <int TEAM, int U>
+template <int TEAM, int U, int ABL = 0>
 static hipError_t launch_c(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, hipStream_t stream) {
@@ -1162,7 +1220,7 @@ static hipError_t launch_c(const uint8_t* arena, uint64_t arena_len, const vpcsu
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_c<TEAM, U, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
+    hipLaunchKernelGGL((k_csum_c<TEAM, U, V, N, ABL>), dim3(g), dim3(256), 0, stream, arena, arena_len,            \
                        (const uint4*)desc, n, out, status, flags_override, arena_w)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -1241,6 +1299,10 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 27: return launch_c<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 28: return launch_c<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 29: return launch_c<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        // ablation builds (wrong results; timing diagnostics only)
+        case 30: return launch_c<8, 12, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 31: return launch_c<8, 12, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 31 + 1: return launch_c<8, 12, 3>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         default: return launch_c<kDefaultTeam, kDefaultUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
     }
 #undef VPC_T
@@ -1485,14 +1547,21 @@ hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const ui
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_read_probe(const uint4* __restrict__ buf, uint64_t n16,
                                                    uint32_t* __restrict__ sink) {
+    // Each workgroup streams one contiguous slab, 8 x 16 B per lane in flight, non-temporal
+    // (the fastest pure-read shape measured by tools/bwlab.hip: ~6.9-7.0 TB/s on MI355X).
     uint32_t x = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * 256u;
-    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const uint4 a = buf[i], b = buf[i + stride], c = buf[i + 2 * stride], d = buf[i + 3 * stride];
-        x ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per;
+    const uint64_t hi = min(lo + per, n16);
+    uint64_t i = lo + threadIdx.x;
+    for (; i + 7 * 256 < hi; i += 8 * 256) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ld_stream<true>(buf + i + u * 256);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     }
-    for (; i < n16; i += stride) {
+    for (; i < hi; i += 256) {
         const uint4 a = buf[i];
         x ^= a.x ^ a.y ^ a.z ^ a.w;
     }
