@@ -83,6 +83,21 @@ def cpu_baseline(workload: str, synth_id: int, stride: int, budget_s: float = 6.
     }
 
 
+def pmc_traffic(workload: str, team: int):
+    """HBM bytes per launch of the default checksum kernel from the newest committed rocprofv3
+    PMC summary (profiles/r*_pmc_<workload>/summary.json, tools/traffic.py: FETCH_SIZE x 2 +
+    WRITE_SIZE per MI355X_MICROARCH.md §HBM).  PMC counters cannot be read from inside this
+    process, so the value comes from that separate --pmc run of the same kernel and config."""
+    import glob
+    if team != 0:
+        return None, None
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{workload}", "summary.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return int(d["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -169,6 +184,7 @@ def main():
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
 
     achieved = bytes_per_step / (kernel_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.workload, args.team)
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -202,7 +218,10 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, corrected)",
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": bytes_per_step,
                 "kernel_avg_ms": round(kernel_ms, 5),
                 "measured_read_ceiling_GBps": round(read_ceiling, 1),
             },

@@ -1,0 +1,144 @@
+package io.vproxy.vpcsum;
+
+import io.vproxy.pni.PNIEnv;
+import io.vproxy.pni.PNILinkOptions;
+import io.vproxy.pni.PanamaUtils;
+
+import java.lang.foreign.MemorySegment;
+import java.lang.invoke.MethodHandle;
+
+/**
+ * Downcalls into libvpcsum.so (MI355X batched Internet checksum), written in the shape the PNI
+ * generator emits for the existing natives (compare
+ * base/src/main/generated/io/vproxy/vfd/posix/PosixNative.java:729-744 in vproxy): one
+ * critical (non-blocking, no upcall) downcall per method, exceptions travel through the PNIEnv
+ * (0 = ok, -1 = exception stored in ENV).  The C side is include/vpcsum.h, symbols
+ * Java_io_vproxy_vpcsum_VPCsum_*.
+ *
+ * Load the library the same way vproxy loads its other natives:
+ * {@code Utils.loadDynamicLibrary("vpcsum")} (base/src/main/java/io/vproxy/base/util/Utils.java:1014-1030).
+ *
+ * Not compiled in this repository (the build image has no JDK); see INTEGRATION.md.
+ */
+public class VPCsum {
+    private VPCsum() {
+    }
+
+    private static final VPCsum INSTANCE = new VPCsum();
+
+    public static VPCsum get() {
+        return INSTANCE;
+    }
+
+    // descriptor flags (include/vpcsum.h)
+    public static final int F_IP = 0x01;
+    public static final int F_L4 = 0x02;
+    public static final int F_RAW = 0x04;
+    // status bits
+    public static final int S_IP_OK = 0x01;
+    public static final int S_L4_OK = 0x02;
+    public static final int S_UDP_NOCSUM = 0x04;
+    public static final int S_DONE = 0x40;
+    public static final int S_BAD_DESC = 0x80;
+    // modes
+    public static final int MODE_COMPUTE = 0x00;
+    public static final int MODE_VERIFY = 0x01;
+    public static final int MODE_WRITE = 0x10;
+
+    private static final MethodHandle createMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(true),
+        "Java_io_vproxy_vpcsum_VPCsum_create", int.class /* device */, long.class /* maxArena */, int.class /* maxPkts */);
+
+    /** Create a context on GPU {@code device}: device buffers for one batch of up to maxPkts
+     * packets spanning at most maxArena bytes (double buffered). Returns an opaque handle. */
+    public long create(PNIEnv ENV, int device, long maxArena, int maxPkts) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) createMH.invokeExact(ENV.MEMORY, device, maxArena, maxPkts);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+        return ENV.returnLong();
+    }
+
+    private static final MethodHandle registerArenaMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(true),
+        "Java_io_vproxy_vpcsum_VPCsum_registerArena", long.class /* ctx */, MemorySegment.class /* arena */, long.class /* len */);
+
+    /** Page-lock a long-lived arena (an AF_XDP umem, UMem.java:36-44) once, so batches from it
+     * DMA straight to the GPU without a staging copy. */
+    public void registerArena(PNIEnv ENV, long ctx, MemorySegment arena, long len) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) registerArenaMH.invokeExact(ENV.MEMORY, ctx, arena, len);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+    }
+
+    private static final MethodHandle submitMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(true),
+        "Java_io_vproxy_vpcsum_VPCsum_submit", long.class /* ctx */, MemorySegment.class /* arena */, long.class /* arenaLen */,
+        MemorySegment.class /* desc */, int.class /* n */, MemorySegment.class /* out */, MemorySegment.class /* status */,
+        int.class /* mode */);
+
+    /** Asynchronously checksum n packets described by 16-byte descriptors (vpcsum_desc_t) over
+     * {@code arena}. Returns a ticket for {@link #waitFor}. */
+    public long submit(PNIEnv ENV, long ctx, MemorySegment arena, long arenaLen, MemorySegment desc, int n,
+                       MemorySegment out, MemorySegment status, int mode) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) submitMH.invokeExact(ENV.MEMORY, ctx, arena, arenaLen, desc, n, out, status, mode);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+        return ENV.returnLong();
+    }
+
+    private static final MethodHandle waitForMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
+        "Java_io_vproxy_vpcsum_VPCsum_waitFor", long.class /* ctx */, long.class /* ticket */);
+
+    /** Block until the batch of {@code ticket} is done; results (and, with MODE_WRITE, the
+     * checksum fields inside the frames) are valid afterwards. Not critical: it may block. */
+    public void waitFor(PNIEnv ENV, long ctx, long ticket) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) waitForMH.invokeExact(ENV.MEMORY, ctx, ticket);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+    }
+
+    private static final MethodHandle closeMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
+        "Java_io_vproxy_vpcsum_VPCsum_close", long.class /* ctx */);
+
+    public void close(PNIEnv ENV, long ctx) {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) closeMH.invokeExact(ENV.MEMORY, ctx);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwLast();
+        }
+    }
+}

@@ -379,3 +379,73 @@ def test_packet_ending_at_unaligned_arena_end(V, orc, team):
             out, st, _ = gpu_compute(V, arena, desc, O.MODE_VERIFY, team)
             oout, ost = orc.process(arena, desc, O.MODE_VERIFY)
             assert np.array_equal(out, oout) and np.array_equal(st, ost), (pad, len(fr))
+
+
+def test_context_sparse_gather_and_zero_copy(V, orc):
+    """Few packets scattered over a large arena: the pageable path gathers only touched blocks;
+    the registered path runs zero-copy (kernel on the host frames, in-place writes)."""
+    big = np.zeros(64 << 20, np.uint8)
+    a_small, d_small = orc.synth(300, 2048, 14, O.SYNTH_FUZZ, O.SEED, 4242)
+    rng = np.random.default_rng(3)
+    slots = np.sort(rng.choice((64 << 20) // 9216 - 1, 300, replace=False))
+    desc = d_small.copy()
+    for i, sl in enumerate(slots):
+        big[sl * 9216: sl * 9216 + 2048] = a_small[i * 2048:(i + 1) * 2048]
+        desc[i]["l3_off"] = sl * 9216 + 14
+    want_out, want_st = orc.process(big, desc, O.MODE_COMPUTE)
+    ctx = V.Context(0, max_arena=1 << 22, max_pkts=1024)     # far smaller than the span
+    out, st = ctx.run(big, desc)
+    assert np.array_equal(out, want_out) and np.array_equal(st, want_st)
+    # zero-copy on the registered arena, with in-place writes
+    want_arena = big.copy()
+    orc.process(want_arena, desc, O.MODE_COMPUTE, write=True)
+    ctx.register(big)
+    out2 = np.zeros(len(desc), np.uint32)
+    ctx.wait(ctx.submit(big, desc, out2, None, O.MODE_WRITE))
+    assert np.array_equal(out2, want_out)
+    assert np.array_equal(big, want_arena)
+    out3, st3 = ctx.run(big, desc, O.MODE_VERIFY)
+    assert np.all(st3 & O.S_L4_OK)
+    ctx.close()
+
+
+def test_egress_batch_mirror(V, orc):
+    """vswitch seam: NAT-style rewrites on the CPU mark sums dirty (setters + checksumSkipped),
+    EgressBatch defers them and flushes once at completeTx; frames must equal Java's full
+    recompute (oracle)."""
+    from vproxy_amd import vswitch as S
+    n, stride = 2000, 2048
+    arena, desc = orc.synth(n, stride, 14, O.SYNTH_C3, O.SEED, 99)
+    orc.process(arena, desc, O.MODE_COMPUTE, write=True)          # valid input checksums
+    rng = np.random.default_rng(8)
+    batch = S.EgressBatch(arena, capacity=256)
+    want = arena.copy()
+    for i in range(n):
+        d = desc[i]
+        l3 = int(d["l3_off"])
+        kind = rng.integers(0, 4)
+        ip_dirty = l4_dirty = False
+        if kind == 1:      # setSrc -> IP dirty + pseudoHeaderChanges (TCP/UDP)
+            new = rng.integers(0, 256, 4, dtype=np.uint8)
+            arena[l3 + 12:l3 + 16] = new
+            want[l3 + 12:l3 + 16] = new
+            ip_dirty = True
+            l4_dirty = int(d["l4_proto"]) in (6, 17)
+        elif kind == 2:    # TTL decrement (IPInputRoute) -> IP dirty
+            arena[l3 + 8] -= 1
+            want[l3 + 8] -= 1
+            ip_dirty = True
+        elif kind == 3 and int(d["l4_proto"]) in (6, 17):   # setDstPort -> L4 dirty
+            arena[l3 + 22:l3 + 24] = [0, 121]
+            want[l3 + 22:l3 + 24] = [0, 121]
+            l4_dirty = True
+        f = S.checksum_flags_for(True, ip_dirty, int(d["l4_proto"]), l4_dirty)
+        if f:
+            one = desc[i:i + 1].copy()
+            one["flags"] = f
+            orc.process(want, one, O.MODE_COMPUTE, write=True)
+        batch.defer(l3, int(d["l3_len"]), int(d["l4_off"]), 4, int(d["l4_proto"]), f)
+    batch.complete_tx()
+    assert batch.stats["tx_csum_gpu"] > 0
+    assert np.array_equal(arena, want)
+    batch.close()

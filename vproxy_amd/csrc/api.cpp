@@ -67,8 +67,12 @@ struct Slot {
     uint32_t* h_out = nullptr;         // pinned staging
     uint8_t* h_status = nullptr;       // pinned staging
     uint8_t* h_arena = nullptr;        // pinned staging for unregistered arenas
+    vpcsum_desc_t* dh_desc = nullptr;  // device-side addresses of the pinned staging
+    uint32_t* dh_out = nullptr;
+    uint8_t* dh_status = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    bool zero_copy = false;            // current batch ran on the host frames in place
     // the batch currently owned by this slot
     uint64_t ticket = 0;
     bool busy = false;
@@ -82,13 +86,19 @@ struct Slot {
 
 }  // namespace vpcsum
 
+struct Registered {
+    uint8_t* host;
+    uint64_t len;
+    uint8_t* dev;    // device-side address of the page-locked mapping (zero-copy access)
+};
+
 struct vpcsum_ctx {
     int device = 0;
     uint64_t max_arena = 0;
     uint32_t max_pkts = 0;
     vpcsum::Slot slots[2];
     uint64_t next_ticket = 1;
-    std::vector<std::pair<uint8_t*, uint64_t>> registered;
+    std::vector<Registered> registered;
     std::mutex mu;
 };
 
@@ -244,9 +254,12 @@ int vpcsum_ctx_create(int device, uint64_t max_arena_bytes, uint32_t max_pkts, v
             (e = hipMalloc((void**)&s.d_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t))) != hipSuccess ||
             (e = hipMalloc((void**)&s.d_out, (size_t)max_pkts * 4)) != hipSuccess ||
             (e = hipMalloc((void**)&s.d_status, (size_t)max_pkts)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t), 0)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_out, (size_t)max_pkts * 4, 0)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_status, (size_t)max_pkts, 0)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t), hipHostMallocMapped)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_out, (size_t)max_pkts * 4, hipHostMallocMapped)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_status, (size_t)max_pkts, hipHostMallocMapped)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&s.dh_desc, s.h_desc, 0)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&s.dh_out, s.h_out, 0)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&s.dh_status, s.h_status, 0)) != hipSuccess ||
             (e = hipHostMalloc((void**)&s.h_arena, max_arena_bytes + 64, 0)) != hipSuccess ||
             (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
@@ -266,7 +279,7 @@ int vpcsum_ctx_destroy(vpcsum_ctx_t* c) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
         slot_free(s);
     }
-    for (auto& r : c->registered) (void)hipHostUnregister(r.first);
+    for (auto& r : c->registered) (void)hipHostUnregister(r.host);
     delete c;
     return 0;
 }
@@ -275,8 +288,14 @@ int vpcsum_ctx_register_arena(vpcsum_ctx_t* c, void* h_arena, uint64_t len) {
     if (!c || !h_arena || len == 0) return fail("vpcsum_ctx_register_arena: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
     VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
-    VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterDefault), "hipHostRegister");
-    c->registered.emplace_back((uint8_t*)h_arena, len);
+    VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterMapped), "hipHostRegister");
+    void* dev = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&dev, h_arena, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(h_arena);
+        return hipfail(e, "hipHostGetDevicePointer");
+    }
+    c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev});
     return 0;
 }
 
@@ -284,7 +303,7 @@ int vpcsum_ctx_unregister_arena(vpcsum_ctx_t* c, void* h_arena) {
     if (!c || !h_arena) return fail("vpcsum_ctx_unregister_arena: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
     for (size_t i = 0; i < c->registered.size(); ++i) {
-        if (c->registered[i].first == (uint8_t*)h_arena) {
+        if (c->registered[i].host == (uint8_t*)h_arena) {
             VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
             c->registered.erase(c->registered.begin() + i);
             return 0;
@@ -293,9 +312,15 @@ int vpcsum_ctx_unregister_arena(vpcsum_ctx_t* c, void* h_arena) {
     return fail("vpcsum_ctx_unregister_arena: arena not registered");
 }
 
-static bool is_registered(vpcsum_ctx* c, const uint8_t* p, uint64_t len) {
+// Device-side address of host range [p, p+len) if it lies in an arena registered with this context.
+static uint8_t* mapped_dev(vpcsum_ctx* c, const uint8_t* p, uint64_t len) {
     for (auto& r : c->registered)
-        if (p >= r.first && p + len <= r.first + r.second) return true;
+        if (p >= r.host && p + len <= r.host + r.len) return r.dev + (p - r.host);
+    return nullptr;
+}
+
+static bool is_registered(vpcsum_ctx* c, const uint8_t* p, uint64_t len) {
+    if (mapped_dev(c, p, len)) return true;
     // page-locked elsewhere (hipHostMalloc, another library's hipHostRegister)?
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost) {
@@ -311,7 +336,7 @@ static int slot_finish(vpcsum_ctx* c, Slot& s) {
     VPC_CHECK(hipEventSynchronize(s.done), "hipEventSynchronize");
     if (s.user_out) memcpy(s.user_out, s.h_out, (size_t)s.n * 4);
     if (s.user_status) memcpy(s.user_status, s.h_status, s.n);
-    if ((s.mode & VPCSUM_MODE_WRITE) && s.user_arena) {
+    if ((s.mode & VPCSUM_MODE_WRITE) && s.user_arena && !s.zero_copy) {
         // place the GPU results into the caller's frames (big endian, as ByteArray.int16)
         for (uint32_t i = 0; i < s.n; ++i) {
             const vpcsum_desc_t& d = s.user_desc[i];
@@ -343,39 +368,75 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
     if (s.busy && slot_finish(c, s) != 0) return -1;
 
     // byte span the descriptors touch (16-B aligned so device alignment == host alignment)
-    uint64_t lo = UINT64_MAX, hi = 0;
+    uint64_t lo = UINT64_MAX, hi = 0, used = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const vpcsum_desc_t& d = h_desc[i];
         if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) continue;   // kernel flags it BAD
         lo = std::min(lo, d.l3_off);
         hi = std::max(hi, d.l3_off + d.l3_len);
+        used += d.l3_len + 16;
     }
     if (lo == UINT64_MAX) { lo = 0; hi = 0; }
     lo &= ~(uint64_t)15;
     const uint64_t span = hi - lo;
-    if (span > c->max_arena) return fail("vpcsum_ctx_submit: batch spans %llu bytes > capacity %llu",
-                                         (unsigned long long)span, (unsigned long long)c->max_arena);
-    // descriptors rebased to the device copy of [lo, hi)
-    for (uint32_t i = 0; i < n; ++i) {
-        s.h_desc[i] = h_desc[i];
-        if (h_desc[i].l3_off >= lo) s.h_desc[i].l3_off = h_desc[i].l3_off - lo;
-        else s.h_desc[i].l3_off = UINT64_MAX;   // out of span -> BAD in the kernel
-    }
-    VPC_CHECK(hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)n * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice, s.stream),
-              "H2D descriptors");
-    if (span) {
-        const uint8_t* src = h_arena + lo;
-        if (!is_registered(c, src, span)) {
-            memcpy(s.h_arena, src, span);   // pageable -> pinned staging
-            src = s.h_arena;
+    s.zero_copy = false;
+
+    uint8_t* dev_arena = span ? mapped_dev(c, h_arena + lo, span) : nullptr;
+    if (dev_arena) {
+        // Zero-copy: the frames live in a page-locked, mapped arena (an AF_XDP umem).  The
+        // kernel reads them over PCIe in place, takes the descriptors from and writes the
+        // results to pinned staging, and with MODE_WRITE stores the checksum fields straight
+        // into the frames -- no DMA copy in either direction.
+        memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
+        uint8_t* base = dev_arena - lo;   // device address of h_arena[0]
+        VPC_CHECK(launch_csum(base, arena_len, s.dh_desc, n, s.dh_out, s.dh_status, nullptr,
+                              mode & VPCSUM_MODE_VERIFY, (mode & VPCSUM_MODE_WRITE) ? base : nullptr, 0, 0, s.stream),
+                  "checksum launch (zero-copy)");
+        s.zero_copy = true;
+    } else {
+        const bool gather = span > 2 * used + (64u << 10);
+        uint64_t dev_len = span;
+        if (gather) {
+            // sparse batch in a large pageable arena: gather the touched 16-B blocks only
+            uint64_t pos = 0;
+            for (uint32_t i = 0; i < n; ++i) {
+                const vpcsum_desc_t& d = h_desc[i];
+                s.h_desc[i] = d;
+                if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) { s.h_desc[i].l3_off = UINT64_MAX; continue; }
+                const uint64_t a0 = d.l3_off & ~(uint64_t)15;
+                const uint64_t a1 = std::min<uint64_t>((d.l3_off + d.l3_len + 15) & ~(uint64_t)15, arena_len);
+                if (pos + (a1 - a0) > c->max_arena) return fail("vpcsum_ctx_submit: gathered batch exceeds capacity");
+                memcpy(s.h_arena + pos, h_arena + a0, a1 - a0);
+                s.h_desc[i].l3_off = pos + (d.l3_off - a0);
+                pos += (a1 - a0 + 15) & ~(uint64_t)15;
+            }
+            dev_len = pos;
+        } else {
+            if (span > c->max_arena) return fail("vpcsum_ctx_submit: batch spans %llu bytes > capacity %llu",
+                                                 (unsigned long long)span, (unsigned long long)c->max_arena);
+            // descriptors rebased to the device copy of [lo, hi)
+            for (uint32_t i = 0; i < n; ++i) {
+                s.h_desc[i] = h_desc[i];
+                if (h_desc[i].l3_off >= lo) s.h_desc[i].l3_off = h_desc[i].l3_off - lo;
+                else s.h_desc[i].l3_off = UINT64_MAX;   // out of span -> BAD in the kernel
+            }
         }
-        VPC_CHECK(hipMemcpyAsync(s.d_arena, src, span, hipMemcpyHostToDevice, s.stream), "H2D arena");
+        VPC_CHECK(hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)n * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice, s.stream),
+                  "H2D descriptors");
+        if (dev_len) {
+            const uint8_t* src = gather ? s.h_arena : h_arena + lo;
+            if (!gather && !is_registered(c, src, span)) {
+                memcpy(s.h_arena, src, span);   // pageable -> pinned staging
+                src = s.h_arena;
+            }
+            VPC_CHECK(hipMemcpyAsync(s.d_arena, src, dev_len, hipMemcpyHostToDevice, s.stream), "H2D arena");
+        }
+        VPC_CHECK(launch_csum(s.d_arena, dev_len, s.d_desc, n, s.d_out, s.d_status, nullptr, mode & VPCSUM_MODE_VERIFY,
+                              nullptr, 0, 0, s.stream),
+                  "checksum launch");
+        VPC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream), "D2H out");
+        VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
     }
-    VPC_CHECK(launch_csum(s.d_arena, span, s.d_desc, n, s.d_out, s.d_status, nullptr, mode & VPCSUM_MODE_VERIFY,
-                          nullptr, 0, 0, s.stream),
-              "checksum launch");
-    VPC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream), "D2H out");
-    VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
     VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
     s.busy = true;
     s.ticket = t;
