@@ -155,10 +155,8 @@ def main():
         dist.barrier()
     kernel_ms = ev0.elapsed_ms(ev1) / args.steps
 
-    wall_t = torch.tensor([wall], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    wall_max = float(wall_t.item())
+    from vproxy_amd.shard import all_ranks_ok, max_over_ranks
+    wall_max = max_over_ranks(wall)
 
     # measured streaming-read ceiling on the same buffer (context for the roofline fraction)
     sink = torch.zeros(8192, dtype=torch.int32, device="cuda")
@@ -179,9 +177,7 @@ def main():
     st = status.cpu().numpy()
     want_ok = np.where(desc_np["flags"] & 1, 1, 0) | np.where(desc_np["flags"] & 2, 2, 0)
     verify_ok = bool(np.all((st & 3) == want_ok))
-    ok_t = torch.tensor([1 if verify_ok else 0], dtype=torch.int32)
-    if world > 1:
-        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+    all_ok = all_ranks_ok(verify_ok)
 
     achieved = bytes_per_step / (kernel_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.workload, args.team)
@@ -210,7 +206,7 @@ def main():
                 "packets_per_gpu": n,
                 "algorithmic_bytes_per_step_per_gpu": bytes_per_step,
                 "parallelism": f"shard-per-GPU x{world} (independent streams, no collective)",
-                "verify_all_packets": bool(ok_t.item()),
+                "verify_all_packets": all_ok,
             },
             "roofline": {
                 "bound": "hbm",
@@ -230,7 +226,7 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if not bool(ok_t.item()):
+    if not all_ok:
         sys.exit(3)
 
 

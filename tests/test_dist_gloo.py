@@ -1,0 +1,75 @@
+"""Multi-rank control plane on CPU (gloo, world size 2): packet sharding is disjoint and
+complete, and bench.py's max-over-ranks timing / all-ranks verify gate reduce correctly.
+The data path itself has no collective."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from vproxy_amd.shard import shard_by_bytes, shard_range
+
+
+def test_shard_range_disjoint_complete():
+    for n in (0, 1, 7, 1000, 1 << 20):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(n, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            for a, b in zip(rs, rs[1:]):
+                assert a[1] == b[0]
+            sizes = [b - a for a, b in rs]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_shard_by_bytes_balanced():
+    rng = np.random.default_rng(1)
+    lens = rng.choice([64, 576, 1500, 9000], 10000)
+    for world in (1, 2, 4, 8):
+        rs = shard_by_bytes(lens, world)
+        assert rs[0][0] == 0 and rs[-1][1] == len(lens)
+        tot = [int(lens[a:b].sum()) for a, b in rs]
+        assert max(tot) - min(tot) <= 2 * 9000
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from vproxy_amd.shard import all_ranks_ok, max_over_ranks, rank_seed_first_index, shard_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.barrier()
+    m = max_over_ranks(float(rank) + 0.5)
+    ok = all_ranks_ok(rank != 1)
+    ok_all = all_ranks_ok(True)
+    lo, hi = shard_range(1000, rank, world)
+    q.put((rank, m, ok, ok_all, lo, hi, rank_seed_first_index(1 << 20, rank)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_reductions():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [1.5, 1.5]                 # max over ranks
+    assert [r[2] for r in res] == [False, False]             # one rank failed -> all fail
+    assert [r[3] for r in res] == [True, True]
+    assert [(r[4], r[5]) for r in res] == [(0, 500), (500, 1000)]
+    assert [r[6] for r in res] == [0, 1 << 20]               # disjoint synthetic sub-streams

@@ -6,4 +6,4 @@ run() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "gpurun_out/$
         echo "rc($name)=$rc"; grep '^{' "gpurun_out/$name.log" | cut -c1-1500; if [ $rc -gt 1 ]; then exit $rc; fi; }
 for w in ${WL:-c1 c3 c4}; do run bench_$w 300 python bench.py --workload $w --steps 100 --warmup 10 --cpu-budget 3; done
 run natbench 200 python tools/natbench.py
-run hostpath 400 python tools/hostpath.py
+[ "${HOSTPATH:-0}" = 1 ] && run hostpath 400 python tools/hostpath.py

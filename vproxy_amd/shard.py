@@ -35,3 +35,25 @@ def rank_seed_first_index(n_per_rank: int, rank: int) -> int:
     """Disjoint synthetic sub-streams per rank: rank r generates packets [r*n, (r+1)*n) of the
     counter-based stream, so every rank's bytes differ and any packet can be regenerated."""
     return n_per_rank * rank
+
+
+def max_over_ranks(x: float) -> float:
+    """Max of a float over all ranks (bench timing); identity without torch.distributed."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(x)
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_ranks_ok(ok: bool) -> bool:
+    """True only if every rank reports ok (bench verify gate)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
