@@ -449,3 +449,16 @@ def test_egress_batch_mirror(V, orc):
     assert batch.stats["tx_csum_gpu"] > 0
     assert np.array_equal(arena, want)
     batch.close()
+
+
+def test_cpp_consumer_runs(V, tmp_path):
+    """Run the plain-C++ C-ABI consumer (ctx API + PNI entry points) on the GPU."""
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "capi_smoke"
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-I", os.path.join(repo, "include"),
+                           os.path.join(repo, "tests", "cpp", "capi_smoke.cpp"), "-L", os.path.join(repo, "vproxy_amd"),
+                           "-lvpcsum", "-Wl,-rpath," + os.path.join(repo, "vproxy_amd"), "-o", str(exe)])
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "capi ok" in r.stdout

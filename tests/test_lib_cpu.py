@@ -69,3 +69,12 @@ def test_descriptor_layout_matches_header():
     assert vpcsum.DESC_DTYPE == O.DESC_DTYPE and vpcsum.DESC_DTYPE.itemsize == 16
     assert vpcsum.NAT4_DTYPE.itemsize == 16
     assert [vpcsum.DESC_DTYPE.fields[k][1] for k in vpcsum.DESC_DTYPE.names] == [0, 8, 10, 12, 13, 14, 15]
+
+
+def test_cpp_consumer_builds(libpath, tmp_path):
+    """The C-ABI is consumable from plain C++ (no torch, no Python): compile + link only."""
+    exe = tmp_path / "capi_smoke"
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(REPO, "include"),
+                           os.path.join(REPO, "tests", "cpp", "capi_smoke.cpp"), "-L", os.path.dirname(libpath),
+                           "-lvpcsum", "-o", str(exe)])
+    assert exe.exists()

@@ -1125,6 +1125,11 @@ __global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ aren
                                 }
                             }
                         }
+                        // Every chunk register counts as consumed on every path.  Without this the
+                        // waitcnt pass keeps the exec-skipped loads "pending" across the back edge
+                        // and puts vmcnt(0) at the loop head, which also drains the next packet's
+                        // descriptor prefetch: one exposed memory latency per packet.
+                        asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
                     }
                 }
             } else {
@@ -1145,6 +1150,7 @@ __global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ aren
                         for (int j = 0; j < 4; ++j)
                             hdr_dword(w[j], c + 4 * j, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
                     }
+                    asm volatile("" ::"v"(vv.x), "v"(vv.y), "v"(vv.z), "v"(vv.w));
                 }
             }
 
