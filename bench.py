@@ -116,7 +116,10 @@ def main():
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
+    # one process per GPU; modulo the visible device count so the multi-rank control path can
+    # also be rehearsed with several ranks on a single-GPU box (identity on an 8-GPU node)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % max(ndev, 1))
     from vproxy_amd import vpcsum as V
     V.lib()
 

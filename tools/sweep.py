@@ -50,7 +50,7 @@ for r in range(args.rounds):
         e1.record()
         ms = e0.elapsed_ms(e1) / args.iters
         res[v].append(nbytes / ms / 1e6)
-        if r == 0 and args.noout in (0, 2) and t < 30:
+        if r == 0 and args.noout in (0, 2) and (t < 30 or t >= 33):
             assert torch.equal(out, ref), f"variant {v} differs"
 print(f"{text}: algorithmic {nbytes / n:.1f} B/pkt")
 for v in variants:

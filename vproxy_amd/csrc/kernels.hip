@@ -545,6 +545,19 @@ __device__ __forceinline__ void hdr_dword(uint32_t w, int d, const PktPlan& pl, 
     }
 }
 
+// Big-endian 16-bit store of a checksum field into a frame, non-temporal (written once; a plain
+// store of a partial line costs far more beside the nt read stream -- measured 2x on k_csum_c).
+__device__ __forceinline__ void st_be16_nt(uint8_t* p, uint32_t v) {
+    typedef __attribute__((address_space(1))) uint16_t g16;
+    typedef __attribute__((address_space(1))) uint8_t g8;
+    if (((uintptr_t)p & 1) == 0) {
+        __builtin_nontemporal_store((uint16_t)(((v & 0xff) << 8) | ((v >> 8) & 0xff)), (g16*)p);
+    } else {
+        __builtin_nontemporal_store((uint8_t)(v >> 8), (g8*)p);
+        __builtin_nontemporal_store((uint8_t)v, (g8*)(p + 1));
+    }
+}
+
 // [lo, hi) as a 32-bit halfword mask (bits clipped to 0..31)
 __device__ __forceinline__ uint32_t hw_range(int lo, int hi) {
     const uint32_t mh = hi >= 32 ? 0xffffffffu : (hi <= 0 ? 0u : ((1u << hi) - 1u));
@@ -974,8 +987,8 @@ __global__ __launch_bounds__(256) void k_csum_b(const uint8_t* __restrict__ aren
 // shuffled to lane (packet - P0) and out/status are written with one 256-B / 64-B store per
 // 64 packets instead of one 4-B / 1-B store per team (the scattered stores cost 3-4% each).
 // ------------------------------------------------------------------------------------------
-template <int TEAM, int U, bool VERIFY, bool NT, int ABL = 0>
-__global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ arena, uint64_t arena_len,
+template <int TEAM, int U, bool VERIFY, bool NT, int ABL = 0, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_c(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
@@ -1189,8 +1202,8 @@ __global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ aren
                     }
                     if (arena_w && tl == 0) {
                         uint8_t* w = arena_w + off;
-                        if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
-                        if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
+                        if (do_ip) st_be16_nt(w + 10, ipc);
+                        if (do_l4) st_be16_nt(w + l4o + fld, l4c);
                     }
                 }
                 ro = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
@@ -1203,7 +1216,7 @@ __global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ aren
             if (lane / PPI == it) { res_out = go; res_st = gs; }
         }
         if (P0 + lane < n) {
-            if (NT) {   // results are written once: stream them past the caches like the reads
+            if (NT && !(ABL & 4)) {   // results are written once: stream them past the caches like the reads
                 if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lane));
                 if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lane));
             } else {
@@ -1214,7 +1227,7 @@ __global__ __launch_bounds__(256) void k_csum_c(const uint8_t* __restrict__ aren
     }
 }
 
-template <int TEAM, int U, int ABL = 0>
+template <int TEAM, int U, int ABL = 0, int WPE = 1>
 static hipError_t launch_c(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, hipStream_t stream) {
@@ -1226,7 +1239,7 @@ static hipError_t launch_c(const uint8_t* arena, uint64_t arena_len, const vpcsu
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_c<TEAM, U, V, N, ABL>), dim3(g), dim3(256), 0, stream, arena, arena_len,            \
+    hipLaunchKernelGGL((k_csum_c<TEAM, U, V, N, ABL, WPE>), dim3(g), dim3(256), 0, stream, arena, arena_len,       \
                        (const uint4*)desc, n, out, status, flags_override, arena_w)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -1309,6 +1322,12 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 30: return launch_c<8, 12, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 31: return launch_c<8, 12, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 31 + 1: return launch_c<8, 12, 3>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        // occupancy targets (waves per SIMD) for the register allocator
+        case 33: return launch_c<8, 6, 0, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 34: return launch_c<8, 6, 0, 7>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 35: return launch_c<8, 6, 0, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 36: return launch_c<4, 12, 0, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 37: return launch_c<8, 6, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         default: return launch_c<kDefaultTeam, kDefaultUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
     }
 #undef VPC_T
