@@ -72,7 +72,7 @@ def pack(frames, infos, stride=None, pad=0):
 
 
 @pytest.mark.parametrize("pad", [0, 1, 2, 3, 14, 15, 398])
-@pytest.mark.parametrize("team", [0, 2, 3, 5, 6, 9, 12, 16, 17, 21, 22, 26, 28, 29])
+@pytest.mark.parametrize("team", [0, 2, 3, 5, 6, 9, 12, 16, 17, 21, 22, 26, 28, 29, 40, 41, 42, 43, 44, 45])
 def test_kats_on_gpu(V, orc, pad, team):
     kats, frames, infos = kat_batch()
     arena, desc = pack(frames, infos, pad=pad)
@@ -129,7 +129,7 @@ def test_synth_matches_oracle_and_checksums(V, orc, workload, pad):
     torch.cuda.synchronize()
     assert np.array_equal(arena.cpu().numpy(), arena_o), "GPU generator differs from oracle generator"
     assert np.array_equal(V.tensor_to_desc(d), desc_o)
-    for team in (0, 2, 6, 12, 16, 21, 26, 29):
+    for team in (0, 2, 6, 12, 16, 21, 26, 29, 40, 41, 43, 45):
         out, st, written = gpu_compute(V, arena_o, desc_o, O.MODE_COMPUTE, team, write=True)
         a2 = arena_o.copy()
         oout, ost = orc.process(a2, desc_o, O.MODE_COMPUTE, write=True)
@@ -143,7 +143,8 @@ def test_synth_matches_oracle_and_checksums(V, orc, workload, pad):
     assert np.array_equal(out2, out)
 
 
-def test_raw_ranges(V, orc):
+@pytest.mark.parametrize("team", [0, 27, 40, 45])
+def test_raw_ranges(V, orc, team):
     rng = np.random.default_rng(5)
     lens = [0, 1, 2, 3, 5, 15, 16, 17, 31, 33, 63, 64, 65, 1499, 1500, 1501, 4097, 9000, 65535]
     arena = rng.integers(0, 256, 200000, dtype=np.uint8)
@@ -155,12 +156,13 @@ def test_raw_ranges(V, orc):
             if off + L <= len(arena):
                 rows.append((off, L, 0, 0, 0, O.F_RAW, 0))
     desc = np.array(rows, dtype=O.DESC_DTYPE)
-    out, st, _ = gpu_compute(V, arena, desc)
+    out, st, _ = gpu_compute(V, arena, desc, team_log2=team)
     for r, o in zip(rows, out):
         assert o == O.csum(arena[r[0]:r[0] + r[1]].tobytes()), r
 
 
-def test_bad_descriptors(V, orc):
+@pytest.mark.parametrize("team", [0, 40])
+def test_bad_descriptors(V, orc, team):
     arena = np.zeros(4096, np.uint8)
     arena[0] = 0x45
     rows = [
@@ -174,11 +176,38 @@ def test_bad_descriptors(V, orc):
         (2 ** 63, 100, 20, 4, 6, 3, 0),  # absurd offset
     ]
     desc = np.array(rows, dtype=O.DESC_DTYPE)
-    out, st, after = gpu_compute(V, arena, desc, write=True)
+    out, st, after = gpu_compute(V, arena, desc, team_log2=team, write=True)
     oout, ost = orc.process(arena.copy(), desc)
     assert np.all(st == O.S_BAD_DESC) and np.all(ost == O.S_BAD_DESC)
     assert np.all(out == 0)
     assert np.array_equal(after, arena)
+
+
+@pytest.mark.parametrize("team", [0, 27, 40, 41, 45])
+@pytest.mark.parametrize("mode", [O.MODE_COMPUTE, O.MODE_VERIFY])
+def test_mixed_batch_bad_raw_interleaved(V, orc, team, mode):
+    """Rejected, raw-range and slow-class (odd offset) descriptors interleaved with ordinary
+    packets inside the same 64-packet groups: the size-sorted kernel must still hand every
+    result back to its own descriptor."""
+    n, stride, pad = 1000, 9088, 14
+    arena, desc = orc.synth(n, stride, pad, O.SYNTH_FUZZ, O.SEED, 4242)
+    orc.process(arena, desc, O.MODE_COMPUTE, write=True)
+    rng = np.random.default_rng(11)
+    pick = rng.random(n)
+    bad = pick < 0.1
+    desc["l3_ver"][bad] = 5
+    raw = (pick >= 0.1) & (pick < 0.2)
+    desc["flags"][raw] = O.F_RAW
+    odd = (pick >= 0.2) & (pick < 0.3)
+    desc["l3_off"][odd] += 1                      # misaligned L3: slow class, garbage but defined
+    desc["l3_len"][odd] = np.minimum(desc["l3_len"][odd], 8000)
+    arena[rng.integers(0, arena.size, 500)] ^= 0x41   # some verify failures
+    out, st, after = gpu_compute(V, arena, desc, mode, team, write=True)
+    a2 = arena.copy()
+    oout, ost = orc.process(a2, desc, mode, write=True)
+    assert np.array_equal(st, ost)
+    assert np.array_equal(out, oout)
+    assert np.array_equal(after, a2)
 
 
 def _nat_batch(orc, n, seed=3, corrupt=0.0, udp_zero=0.0):
@@ -365,7 +394,7 @@ def test_full_size_c2_properties(V, orc):
         assert o[i] == w[0]
 
 
-@pytest.mark.parametrize("team", [0, 3, 9, 21, 26])
+@pytest.mark.parametrize("team", [0, 3, 9, 21, 26, 40, 45])
 def test_packet_ending_at_unaligned_arena_end(V, orc, team):
     """Arena length not a multiple of 16 and the last packet ending exactly at the arena end:
     the final partial chunk must still be read (buffer-descriptor range rounding)."""

@@ -123,15 +123,16 @@ int vpcsum_set_device(int device) {
     return 0;
 }
 
-static int team_from_mode(uint32_t mode) { return (int)((mode >> 8) & 0x1f); }
+// kernel variant id: bits 8..12 low, bits 24..26 high (0..255; 0 = default)
+static int team_from_mode(uint32_t mode) { return (int)(((mode >> 8) & 0x1f) | (((mode >> 24) & 0x7) << 5)); }
 
 int vpcsum_compute_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, uint32_t n,
                          uint32_t* d_out, uint8_t* d_status, uint32_t mode, void* stream) {
     if (n == 0) return 0;
     if (!d_arena || !d_desc) return fail("vpcsum_compute_async: NULL arena or descriptors");
-    // tuning hints (not part of the stable ABI): bits 8..12 kernel variant, bit 13 plain
-    // (temporal) loads, bits 16..23 workgroups per CU.
-    if (mode & ~(0x00ff3fffu | VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_compute_async: bad mode 0x%x", mode);
+    // tuning hints (not part of the stable ABI): bits 8..12 + 24..26 kernel variant, bit 13
+    // plain (temporal) loads, bits 16..23 workgroups per CU.
+    if (mode & ~(0x07ff3fffu | VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_compute_async: bad mode 0x%x", mode);
     uint8_t* w = (mode & VPCSUM_MODE_WRITE) ? const_cast<uint8_t*>(d_arena) : nullptr;
     int grid = 0;
     if ((mode >> 16) & 0xff) {

@@ -1250,6 +1250,309 @@ static hipError_t launch_c(const uint8_t* arena, uint64_t arena_len, const vpcsu
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// K2: owner-lane plans, size-sorted teams.  A wave takes 64 consecutive packets per
+// super-iteration.  Lane L decodes descriptor P0+L once (validation, chunk plan, header
+// bitmaps), ranks its packet by cost class with ballots and publishes the plan to LDS slot
+// `rank`.  Then TEAM iterations: team t of iteration `it` streams the packet of slot
+// it*PPI+t and leaves its partial sums in that slot.  Last, lane L reads its slot back and
+// finalizes its own packet; out/status are written coalesced.  Decode and finalize are
+// issued once per 64 packets instead of TEAM times (K1 repeats them in every team lane),
+// and the sort puts packets of similar length in the same iteration, so a ragged batch
+// (C3) no longer pays the longest of PPI random packets per iteration.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int TEAM, int U, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                const uint4* __restrict__ desc, uint32_t n,
+                                                uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                                const uint8_t* __restrict__ flags_override,
+                                                uint8_t* __restrict__ arena_w) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    constexpr int PPI = 64 / TEAM;   // packets per iteration per wave
+    // slot: q0 {boff, nch | klo<<16 | do_ip<<30 | fast<<31, kfast, l4hi}, q1 bitmaps,
+    // q2/q3 the byte-range plan of the slow class; q0 is overwritten with the team's sums.
+    __shared__ uint4 s_slot[4][64][4];
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int tl = lane & (TEAM - 1);
+    const int tid = lane / TEAM;
+    const uint32_t gw = (blockIdx.x * 256u + threadIdx.x) >> 6;
+    const uint32_t wstride = gridDim.x * 4u * 64u;
+
+    uint32_t P0 = gw * 64u;
+    uint4 dnext = make_uint4(0, 0, 0, 0);
+    int fnext = 0;
+    if (P0 + lane < n) {
+        dnext = desc[P0 + lane];
+        if (flags_override) fnext = flags_override[P0 + lane];
+    }
+    for (; P0 < n; P0 += wstride) {
+        // ---- phase A: this lane's packet ----
+        const uint4 dv = dnext;
+        const int fov = fnext;
+        {
+            const uint32_t q = P0 + wstride + lane;
+            if (q < n) {
+                dnext = desc[q];
+                if (flags_override) fnext = flags_override[q];
+            }
+        }
+        const bool live = P0 + lane < n;
+        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        const int len = dv.z & 0xffff;
+        const int l4o = dv.z >> 16;
+        const int ver = dv.w & 0xff;
+        const int proto = (dv.w >> 8) & 0xff;
+        const int fl = flags_override ? fov : (int)((dv.w >> 16) & 0xff);
+
+        bool bad = !live || off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
+        const bool raw = (fl & VPCSUM_F_RAW) != 0;
+        bool do_ip = false, do_l4 = false;
+        int fld = -1;
+        if (!bad && !raw) {
+            if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
+            else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
+            else bad = true;
+            if (!bad && (fl & VPCSUM_F_L4)) {
+                fld = l4_field(proto);
+                if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
+                else do_l4 = true;
+            }
+            if (!bad && (fl & VPCSUM_F_IP)) {
+                if (ver != 4) bad = true;
+                else do_ip = true;
+            }
+        }
+        const int r0 = (int)(off & 15);
+        int key = 0;
+        {
+            PktPlan pl;
+            pl.r0 = r0;
+            const uint32_t boff = (uint32_t)(off & ~(uint64_t)15);
+            const int need = bad ? 0 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
+            pl.nch = bad ? 0 : (r0 + need + 15) >> 4;
+            if (raw) {
+                pl.l4lo = r0; pl.l4hi = r0 + len; pl.fa = -64;
+                pl.fast_lo = (r0 + 15) & ~15;
+            } else if (do_l4) {
+                pl.l4lo = r0 + l4o; pl.l4hi = r0 + len; pl.fa = r0 + l4o + fld;
+                pl.fast_lo = (pl.fa + 2 + 15) & ~15;
+            } else {
+                pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
+                pl.fast_lo = 1 << 30;
+            }
+            pl.fast_hi = (r0 + need) & ~15;
+            if (do_ip) { pl.iplo = r0; pl.iphi = r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
+            if (do_l4 && proto != 1) {
+                pl.pslo = r0 + (ver == 4 ? 12 : 8);
+                pl.pshi = r0 + (ver == 4 ? 20 : 40);
+            } else { pl.pslo = 0; pl.pshi = 0; }
+            const int klo = min(pl.fast_lo >> 4, pl.nch);
+            const uint32_t kfast = (uint32_t)max((pl.fast_hi >> 4) - klo, 0);
+            const bool hbm = !raw && !(r0 & 1) && !(l4o & 1) && ((((r0 + need) & 1) == 0) || r0 + need >= 64);
+            uint32_t B_ip = 0, B_l4 = 0, F_ip = 0, F_l4 = 0;
+            if (hbm) {
+                const int r0h = r0 >> 1;
+                if (do_ip) {
+                    F_ip = 1u << (r0h + 5);
+                    B_ip = hw_range(r0h, r0h + (l4o >> 1)) & ~F_ip;
+                }
+                if (do_l4) {
+                    F_l4 = hw_bit(pl.fa >> 1);
+                    B_l4 = hw_range((r0 + l4o) >> 1, (r0 + need + 1) >> 1) & ~F_l4;
+                    if (proto != 1) B_l4 |= (ver == 4) ? hw_range(r0h + 6, r0h + 10) : hw_range(r0h + 4, r0h + 20);
+                }
+            }
+            const bool fastc = hbm && klo <= 4;
+            // cost class: trips of the team loop (fast class), slow class last, bad first
+            if (!bad) key = fastc ? 1 + min((pl.nch + TEAM * U - 1) / (TEAM * U), 13) : 15;
+            uint32_t rank = 0, cnt = 0;
+            for (int b = 0; b < 16 && cnt < 64; ++b) {
+                const uint64_t m = __ballot(key == b);
+                if (key == b)
+                    rank = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                cnt += (uint32_t)__popcll(m);
+            }
+            key = (int)rank;   // from here on: this packet's slot
+            uint4* sl = s_slot[wid][rank];
+            sl[0] = make_uint4(boff, (uint32_t)pl.nch | ((uint32_t)klo << 16) | ((uint32_t)do_ip << 30) | ((uint32_t)fastc << 31),
+                               kfast, (uint32_t)pl.l4hi);
+            sl[1] = make_uint4(B_ip, B_l4, F_ip, F_l4);
+            if (!fastc) {
+                sl[2] = make_uint4((uint32_t)r0, (uint32_t)pl.l4lo, (uint32_t)pl.fa, (uint32_t)pl.iphi);
+                sl[3] = make_uint4((uint32_t)pl.iplo, (uint32_t)pl.pslo, (uint32_t)pl.pshi, 0u);
+            }
+        }
+        wave_sync_lds();
+
+        // ---- phase B: teams stream the packets in slot order ----
+#pragma unroll 1
+        for (int it = 0; it < TEAM; ++it) {
+            uint4* sl = s_slot[wid][it * PPI + tid];
+            const uint4 a = sl[0];
+            const uint32_t boff = a.x;
+            const int nch = (int)(a.y & 0xffff);
+            const int klo = (int)((a.y >> 16) & 0x3fff);
+            const uint32_t kfast = a.z;
+            const int l4hi = (int)a.w;
+            uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
+            uint32_t st_ip = 0, st_l4 = 0;
+            if (a.y >> 31) {
+                const uint4 bm = sl[1];
+                for (int rr = 0; rr * TEAM < nch; rr += U) {
+                    v4u v[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int k = (rr + u) * TEAM + tl;
+                        const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
+                        v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int k = (rr + u) * TEAM + tl;
+                        if ((uint32_t)(k - klo) < kfast) {
+                            acc_l4 += (uint64_t)v[u].x + v[u].y;
+                            acc_l4 += (uint64_t)v[u].z + v[u].w;
+                        } else if (k >= klo) {
+                            const int c = k << 4;
+                            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
+                        } else if (u == 0) {
+                            const int hb0 = k << 3;
+                            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const int hb = hb0 + 2 * j;
+                                acc_ip += w[j] & hmask((bm.x >> hb) & 3);
+                                acc_l4 += w[j] & hmask((bm.y >> hb) & 3);
+                                if (VERIFY) {
+                                    st_ip += w[j] & hmask((bm.z >> hb) & 3);
+                                    st_l4 += w[j] & hmask((bm.w >> hb) & 3);
+                                }
+                            }
+                        }
+                        asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
+                    }
+                }
+            } else if (nch > 0) {
+                const uint4 q2 = sl[2], q3 = sl[3];
+                PktPlan pl;
+                pl.r0 = (int)q2.x; pl.l4lo = (int)q2.y; pl.fa = (int)q2.z; pl.iphi = (int)q2.w;
+                pl.iplo = (int)q3.x; pl.pslo = (int)q3.y; pl.pshi = (int)q3.z;
+                pl.l4hi = l4hi; pl.nch = nch;
+                const bool dip = (a.y >> 30) & 1;
+                for (int r = 0; r * TEAM < nch; ++r) {
+                    const int k = r * TEAM + tl;
+                    const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
+                    const v4u vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+                    const int c = k << 4;
+                    const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+                    if ((uint32_t)(k - klo) < kfast) {
+                        acc_l4 += (uint64_t)w[0] + w[1];
+                        acc_l4 += (uint64_t)w[2] + w[3];
+                    } else if (k >= klo) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            hdr_dword(w[j], c + 4 * j, pl, dip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
+                    }
+                    asm volatile("" ::"v"(vv.x), "v"(vv.y), "v"(vv.z), "v"(vv.w));
+                }
+            }
+            const uint32_t s_l4 = fold32(team_sum<TEAM>(fold64(acc_l4)));
+            const uint32_t s_ip = fold32(team_sum<TEAM>(fold64(acc_ip)));
+            const uint32_t s_ps = fold32(team_sum<TEAM>(fold64(acc_ps)));
+            uint32_t s_st = 0;
+            if (VERIFY) s_st = fold32(team_sum<TEAM>(fold32(st_l4))) | (fold32(team_sum<TEAM>(fold32(st_ip))) << 16);
+            if (tl == 0) sl[0] = make_uint4(s_l4, s_ip, s_ps, s_st);
+        }
+        wave_sync_lds();
+
+        // ---- phase C: finalize this lane's packet ----
+        uint32_t res_out = 0, res_st = VPCSUM_S_BAD_DESC;
+        {
+            const uint4 sums = s_slot[wid][key][0];
+            if (!bad) {
+                uint32_t ipc = 0, l4c = 0;
+                uint32_t st = VPCSUM_S_DONE;
+                if (raw) {
+                    ipc = 0xffff - orient(sums.x, r0);
+                } else {
+                    if (do_ip) ipc = 0xffff - orient(sums.y, r0);
+                    if (do_l4) {
+                        uint32_t tot = orient(sums.x, r0 + l4o);
+                        if (proto != 1) {
+                            const uint32_t l4len = (uint32_t)(len - l4o);
+                            tot += orient(sums.z, r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
+                        }
+                        l4c = 0xffff - fold32(tot);
+                        if (proto == 17 && l4c == 0) l4c = 0xffff;
+                    }
+                    if (VERIFY) {
+                        if (do_ip && orient(sums.w >> 16, r0) == ipc) st |= VPCSUM_S_IP_OK;
+                        if (do_l4) {
+                            const uint32_t stored = orient(sums.w & 0xffff, r0 + l4o + fld);
+                            if (stored == l4c) st |= VPCSUM_S_L4_OK;
+                            if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                        }
+                    }
+                    if (arena_w) {
+                        uint8_t* w = arena_w + off;
+                        if (do_ip) st_be16_nt(w + 10, ipc);
+                        if (do_l4) st_be16_nt(w + l4o + fld, l4c);
+                    }
+                }
+                res_out = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
+                res_st = st;
+            }
+        }
+        if (live) {
+            if (NT) {
+                if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lane));
+                if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lane));
+            } else {
+                if (out) out[P0 + lane] = res_out;
+                if (status) status[P0 + lane] = (uint8_t)res_st;
+            }
+        }
+        wave_sync_lds();   // slots are rewritten by the next super-iteration
+    }
+}
+
+template <int TEAM, int U>
+static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
+                           uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
+                           uint8_t* arena_w, int grid, hipStream_t stream) {
+    if (arena_len > kMaxBufArena || ((uintptr_t)arena & 15))
+        return launch_team<TEAM, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w,
+                                    grid, stream);
+    uint32_t need = (n + 255) / 256;   // 4 waves x 64 packets per workgroup
+    uint32_t g = grid > 0 ? (uint32_t)grid : need;
+    if (g > need) g = need;
+    if (g == 0) g = 1;
+#define VPC_LAUNCH(V, N)                                                                                         \
+    hipLaunchKernelGGL((k_csum_d<TEAM, U, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
+                       (const uint4*)desc, n, out, status, flags_override, arena_w)
+    if (verify) {
+        if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
+    } else {
+        if (nt) VPC_LAUNCH(false, true); else VPC_LAUNCH(false, false);
+    }
+#undef VPC_LAUNCH
+    return hipGetLastError();
+}
+
 template <int TEAM, int U>
 static hipError_t launch_b(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
@@ -1328,6 +1631,12 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 35: return launch_c<8, 6, 0, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 36: return launch_c<4, 12, 0, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 37: return launch_c<8, 6, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 40: return launch_d<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 41: return launch_d<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 42: return launch_d<4, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 43: return launch_d<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 44: return launch_d<8, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 45: return launch_d<2, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         default: return launch_c<kDefaultTeam, kDefaultUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
     }
 #undef VPC_T
