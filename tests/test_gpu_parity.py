@@ -210,10 +210,26 @@ def test_mixed_batch_bad_raw_interleaved(V, orc, team, mode):
     assert np.array_equal(after, a2)
 
 
-def _nat_batch(orc, n, seed=3, corrupt=0.0, udp_zero=0.0):
-    arena, desc = orc.synth(n, 2048, 0, O.SYNTH_C3, O.SEED, 777)
+def _nat_batch(orc, n, seed=3, corrupt=0.0, udp_zero=0.0, pad=0, workload=O.SYNTH_C3, packed=False):
+    stride = 9088 if workload == O.SYNTH_FUZZ else 2048
+    arena, desc = orc.synth(n, stride, pad, workload, O.SEED, 777)
     orc.process(arena, desc, O.MODE_COMPUTE, write=True)       # valid input checksums
     rng = np.random.default_rng(seed)
+    if packed:   # packets back to back (0-3 byte gaps): stores must never spill into a neighbour
+        parts, offs, pos = [], [], pad
+        parts.append(np.zeros(pad, np.uint8))
+        for i in range(n):
+            o, L = int(desc[i]["l3_off"]), int(desc[i]["l3_len"])
+            offs.append(pos)
+            parts.append(arena[o:o + L])
+            gap = int(rng.integers(0, 4))
+            parts.append(rng.integers(0, 256, gap, dtype=np.uint8))
+            pos += L + gap
+        arena = np.concatenate(parts)
+        desc = desc.copy()
+        desc["l3_off"] = offs
+    if workload != O.SYNTH_C3:
+        udp_zero = 0.0
     rw = np.zeros(n, O.NAT4_DTYPE)
     rw["src"] = rng.integers(0, 256, (n, 4))
     rw["dst"] = rng.integers(0, 256, (n, 4))
@@ -230,6 +246,25 @@ def _nat_batch(orc, n, seed=3, corrupt=0.0, udp_zero=0.0):
             arena[l3 + 26] = 0
             arena[l3 + 27] = 0
     return arena, desc, rw
+
+
+@pytest.mark.parametrize("pad", [0, 1, 2, 14, 15])
+@pytest.mark.parametrize("workload", [O.SYNTH_C1, O.SYNTH_C3, O.SYNTH_FUZZ])
+@pytest.mark.parametrize("packed", [False, True])
+def test_nat_wide_and_scalar_kernels(V, orc, pad, workload, packed):
+    """Both NAT kernels (wide LDS-staged and byte-access, nat_mode bit 8) against the Java
+    restatement, at every window alignment, with packets packed back to back."""
+    n = 1500 if workload == O.SYNTH_FUZZ else 3000
+    arena, desc, rw = _nat_batch(orc, n, seed=pad + 17, udp_zero=0.1, pad=pad, workload=workload, packed=packed)
+    want = arena.copy()
+    orc.nat4_java(want, desc, rw)
+    for force_scalar in (0, 0x100):
+        got, st = _gpu_nat(V, arena, desc, rw, V.NAT_RFC1624 | force_scalar)
+        v4 = desc["l3_ver"] == 4
+        assert np.all(st[v4] == O.S_DONE) and np.all(st[~v4] == O.S_BAD_DESC)
+        assert np.array_equal(got, want), force_scalar
+        got, _ = _gpu_nat(V, arena, desc, rw, V.NAT_STRICT_JAVA | force_scalar)
+        assert np.array_equal(got, want), force_scalar
 
 
 def _gpu_nat(V, arena_np, desc, rw, mode):

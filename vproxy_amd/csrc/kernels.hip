@@ -1659,7 +1659,7 @@ __device__ uint32_t lane_sum_range(const uint8_t* lo_p, const uint8_t* hi_p, con
     const uintptr_t a = lo & ~(uintptr_t)3;
     uint64_t acc = 0;
     for (uintptr_t d = a; d < hi; d += 4) {
-        const uint32_t w = *(const uint32_t*)d;
+        const uint32_t w = *(const __attribute__((address_space(1))) uint32_t*)d;
         const int rd = (int)(d - a);
         uint32_t m = bmask(rd, (int)(lo - a), (int)(hi - a));
         if (fld_p) m &= ~bmask(rd, (int)(fa - a), (int)(fa - a) + 2);
@@ -1668,102 +1668,259 @@ __device__ uint32_t lane_sum_range(const uint8_t* lo_p, const uint8_t* hi_p, con
     return fold64(acc);
 }
 
+// One packet, byte accesses (IPv4 options, arenas the buffer path cannot address, or when the
+// wide kernel is disabled).
+__device__ void nat4_scalar(uint8_t* __restrict__ arena, uint64_t arena_len, const vpcsum_desc_t& d,
+                            const vpcsum_nat4_t& r, uint32_t p, uint8_t* __restrict__ status,
+                            uint8_t* __restrict__ flags_out, int strict) {
+    const uint64_t off = d.l3_off;
+    const int len = d.l3_len, l4o = d.l4_off;
+    if (off > arena_len || (uint64_t)len > arena_len - off || d.l3_ver != 4 || len < 20 || l4o < 20 ||
+        l4o > len || (l4o & 3)) {
+        if (status) status[p] = VPCSUM_S_BAD_DESC;
+        if (flags_out) flags_out[p] = kFlagRejected;
+        return;
+    }
+    uint8_t* l3 = arena + off;
+    const int proto = d.l4_proto;
+    const int fld = (proto == 6 || proto == 17) ? l4_field(proto) : -1;
+    const bool l4 = fld >= 0 && len - l4o >= fld + 2;
+    uint8_t* l4p = l3 + l4o;
+
+    // old / new 16-bit words; ip: header words, ps: pseudo words (+ ports for l4)
+    uint32_t ip_diff = 0;   // sum of ~m + m' over changed IP header words
+    uint32_t l4_diff = 0;   // sum of ~m + m' over changed pseudo/L4 words
+    bool ip_dirty = false, l4_dirty = false;
+    if (r.mask & VPCSUM_NAT_SRC) {
+        for (int i = 0; i < 2; ++i) {
+            const uint32_t m = ld16(l3 + 12 + 2 * i);
+            const uint32_t mn = ((uint32_t)r.src[2 * i] << 8) | r.src[2 * i + 1];
+            ip_diff += (~m & 0xffff) + mn;
+            l4_diff += (~m & 0xffff) + mn;
+            st16(l3 + 12 + 2 * i, mn);
+        }
+        ip_dirty = true; l4_dirty = true;
+    }
+    if (r.mask & VPCSUM_NAT_DST) {
+        for (int i = 0; i < 2; ++i) {
+            const uint32_t m = ld16(l3 + 16 + 2 * i);
+            const uint32_t mn = ((uint32_t)r.dst[2 * i] << 8) | r.dst[2 * i + 1];
+            ip_diff += (~m & 0xffff) + mn;
+            l4_diff += (~m & 0xffff) + mn;
+            st16(l3 + 16 + 2 * i, mn);
+        }
+        ip_dirty = true; l4_dirty = true;
+    }
+    if (r.mask & VPCSUM_NAT_DEC_TTL) {
+        const uint32_t m = ld16(l3 + 8);
+        const uint32_t mn = (((m >> 8) - 1) & 0xff) << 8 | (m & 0xff);
+        ip_diff += (~m & 0xffff) + mn;
+        st16(l3 + 8, mn);
+        ip_dirty = true;
+    }
+    if (l4) {
+        if (r.mask & VPCSUM_NAT_SPORT) {
+            const uint32_t m = ld16(l4p);
+            const uint32_t mn = ((uint32_t)r.sport[0] << 8) | r.sport[1];
+            l4_diff += (~m & 0xffff) + mn;
+            st16(l4p, mn);
+            l4_dirty = true;
+        }
+        if (r.mask & VPCSUM_NAT_DPORT) {
+            const uint32_t m = ld16(l4p + 2);
+            const uint32_t mn = ((uint32_t)r.dport[0] << 8) | r.dport[1];
+            l4_diff += (~m & 0xffff) + mn;
+            st16(l4p + 2, mn);
+            l4_dirty = true;
+        }
+    } else {
+        l4_dirty = false;
+    }
+    uint8_t fl = (ip_dirty ? VPCSUM_F_IP : 0) | (l4_dirty ? VPCSUM_F_L4 : 0);
+    if (strict) {
+        // Java semantics for any input: the csum kernel recomputes the dirty sums in full.
+        if (flags_out) flags_out[p] = fl;
+        return;
+    }
+    if (ip_dirty) {
+        const uint32_t hc = ld16(l3 + 10);
+        const uint32_t s = fold32((~hc & 0xffff) + fold32(ip_diff));
+        st16(l3 + 10, ~s & 0xffff);
+    }
+    if (l4_dirty) {
+        const uint32_t hc = ld16(l4p + fld);
+        uint32_t c;
+        if (proto == 17 && hc == 0) {
+            // "no checksum" UDP: Java recomputes the full sum (UdpPacket.java:136-149)
+            const uint32_t seg = orient(lane_sum_range(l4p, l3 + len, l4p + fld), (int)((uintptr_t)l4p & 1));
+            const uint32_t ps = orient(lane_sum_range(l3 + 12, l3 + 20, nullptr), (int)((uintptr_t)l3 & 1));
+            const uint32_t l4len = (uint32_t)(len - l4o);
+            c = 0xffff - fold32(seg + ps + 17u + l4len);
+        } else {
+            const uint32_t s = fold32((~hc & 0xffff) + fold32(l4_diff));
+            c = ~s & 0xffff;
+        }
+        if (proto == 17 && c == 0) c = 0xffff;
+        st16(l4p + fld, c);
+    }
+    if (status) status[p] = VPCSUM_S_DONE;
+}
+
 __global__ __launch_bounds__(256) void k_nat4(uint8_t* __restrict__ arena, uint64_t arena_len,
                                              const vpcsum_desc_t* __restrict__ desc,
                                              const vpcsum_nat4_t* __restrict__ rw, uint32_t n,
                                              uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out,
                                              int strict) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x)
+        nat4_scalar(arena, arena_len, desc[p], rw[p], p, status, flags_out, strict);
+}
+
+// Wide form (IPv4 without options, the C5 shape): the 64-B window holding bytes [8, 40) of the
+// packet is read with four 16-B buffer loads, staged in this lane's LDS slot, rewritten there
+// with byte-addressed LDS ops (the window's offset differs per packet), and the changed dwords
+// [8, 24) and the L4 checksum field are stored back as aligned dwords.  The scalar form needs
+// ~20 byte loads and ~20 byte stores per packet, each one wave instruction touching 64 lines.
+__device__ __forceinline__ uint32_t lds16(const uint8_t* w, int q) { return ((uint32_t)w[q] << 8) | w[q + 1]; }
+__device__ __forceinline__ void sts16(uint8_t* w, int q, uint32_t v) { w[q] = (uint8_t)(v >> 8); w[q + 1] = (uint8_t)v; }
+
+template <bool STRICT>
+__global__ __launch_bounds__(256) void k_nat4w(uint8_t* __restrict__ arena, uint64_t arena_len,
+                                              const vpcsum_desc_t* __restrict__ desc,
+                                              const vpcsum_nat4_t* __restrict__ rw, uint32_t n,
+                                              uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    // 72-B slot per lane (64-B window + 8): an 18-dword stride keeps byte ops <= 2-way on banks
+    __shared__ uint2 s_win[256][9];
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
+    uint8_t* w = (uint8_t*)&s_win[threadIdx.x][0];
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
-        const vpcsum_desc_t d = desc[p];
-        const vpcsum_nat4_t r = rw[p];
-        const uint64_t off = d.l3_off;
-        const int len = d.l3_len, l4o = d.l4_off;
-        if (off > arena_len || (uint64_t)len > arena_len - off || d.l3_ver != 4 || len < 20 || l4o < 20 ||
-            l4o > len || (l4o & 3)) {
-            if (status) status[p] = VPCSUM_S_BAD_DESC;
-            if (flags_out) flags_out[p] = kFlagRejected;
+        const uint4 dv = ((const uint4*)desc)[p];
+        const uint4 rv = ((const uint4*)rw)[p];
+        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        const int len = dv.z & 0xffff, l4o = dv.z >> 16;
+        const int ver = dv.w & 0xff, proto = (dv.w >> 8) & 0xff;
+        if (l4o != 20 || ver != 4 || off > arena_len || (uint64_t)len > arena_len - off || len < 20) {
+            nat4_scalar(arena, arena_len, desc[p], rw[p], p, status, flags_out, STRICT ? 1 : 0);
             continue;
         }
-        uint8_t* l3 = arena + off;
-        const int proto = d.l4_proto;
+        const int mask = rv.w & 0xff;
         const int fld = (proto == 6 || proto == 17) ? l4_field(proto) : -1;
-        const bool l4 = fld >= 0 && len - l4o >= fld + 2;
-        uint8_t* l4p = l3 + l4o;
-
-        // old / new 16-bit words; ip: header words, ps: pseudo words (+ ports for l4)
-        uint32_t ip_diff = 0;   // sum of ~m + m' over changed IP header words
-        uint32_t l4_diff = 0;   // sum of ~m + m' over changed pseudo/L4 words
+        const bool l4 = fld >= 0 && len - 20 >= fld + 2;
+        const int r0 = (int)(off & 15);
+        const uint32_t boff = (uint32_t)(off - (uint64_t)r0);
+        const int wend = r0 + (l4 ? 22 + fld : 24);   // window bytes needed
+        {
+            v4u v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                v[k] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (k << 4) < wend ? boff + (k << 4) : kOutOfRange, 0, 0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                s_win[threadIdx.x][2 * k] = make_uint2(v[k].x, v[k].y);
+                s_win[threadIdx.x][2 * k + 1] = make_uint2(v[k].z, v[k].w);
+            }
+        }
+        const int b = r0;   // packet byte 0 inside the window
+        uint32_t ip_diff = 0, l4_diff = 0;
         bool ip_dirty = false, l4_dirty = false;
-        if (r.mask & VPCSUM_NAT_SRC) {
+        if (mask & VPCSUM_NAT_SRC) {
+#pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const uint32_t m = ld16(l3 + 12 + 2 * i);
-                const uint32_t mn = ((uint32_t)r.src[2 * i] << 8) | r.src[2 * i + 1];
+                const uint32_t m = lds16(w, b + 12 + 2 * i);
+                const uint32_t mn = (((rv.x >> (16 * i)) & 0xff) << 8) | ((rv.x >> (16 * i + 8)) & 0xff);
                 ip_diff += (~m & 0xffff) + mn;
                 l4_diff += (~m & 0xffff) + mn;
-                st16(l3 + 12 + 2 * i, mn);
+                sts16(w, b + 12 + 2 * i, mn);
             }
             ip_dirty = true; l4_dirty = true;
         }
-        if (r.mask & VPCSUM_NAT_DST) {
+        if (mask & VPCSUM_NAT_DST) {
+#pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const uint32_t m = ld16(l3 + 16 + 2 * i);
-                const uint32_t mn = ((uint32_t)r.dst[2 * i] << 8) | r.dst[2 * i + 1];
+                const uint32_t m = lds16(w, b + 16 + 2 * i);
+                const uint32_t mn = (((rv.y >> (16 * i)) & 0xff) << 8) | ((rv.y >> (16 * i + 8)) & 0xff);
                 ip_diff += (~m & 0xffff) + mn;
                 l4_diff += (~m & 0xffff) + mn;
-                st16(l3 + 16 + 2 * i, mn);
+                sts16(w, b + 16 + 2 * i, mn);
             }
             ip_dirty = true; l4_dirty = true;
         }
-        if (r.mask & VPCSUM_NAT_DEC_TTL) {
-            const uint32_t m = ld16(l3 + 8);
+        if (mask & VPCSUM_NAT_DEC_TTL) {
+            const uint32_t m = lds16(w, b + 8);
             const uint32_t mn = (((m >> 8) - 1) & 0xff) << 8 | (m & 0xff);
             ip_diff += (~m & 0xffff) + mn;
-            st16(l3 + 8, mn);
+            sts16(w, b + 8, mn);
             ip_dirty = true;
         }
         if (l4) {
-            if (r.mask & VPCSUM_NAT_SPORT) {
-                const uint32_t m = ld16(l4p);
-                const uint32_t mn = ((uint32_t)r.sport[0] << 8) | r.sport[1];
+            if (mask & VPCSUM_NAT_SPORT) {
+                const uint32_t m = lds16(w, b + 20);
+                const uint32_t mn = ((rv.z & 0xff) << 8) | ((rv.z >> 8) & 0xff);
                 l4_diff += (~m & 0xffff) + mn;
-                st16(l4p, mn);
+                sts16(w, b + 20, mn);
                 l4_dirty = true;
             }
-            if (r.mask & VPCSUM_NAT_DPORT) {
-                const uint32_t m = ld16(l4p + 2);
-                const uint32_t mn = ((uint32_t)r.dport[0] << 8) | r.dport[1];
+            if (mask & VPCSUM_NAT_DPORT) {
+                const uint32_t m = lds16(w, b + 22);
+                const uint32_t mn = (((rv.z >> 16) & 0xff) << 8) | ((rv.z >> 24) & 0xff);
                 l4_diff += (~m & 0xffff) + mn;
-                st16(l4p + 2, mn);
+                sts16(w, b + 22, mn);
                 l4_dirty = true;
             }
         } else {
             l4_dirty = false;
         }
-        uint8_t fl = (ip_dirty ? VPCSUM_F_IP : 0) | (l4_dirty ? VPCSUM_F_L4 : 0);
-        if (strict) {
-            // Java semantics for any input: the csum kernel recomputes the dirty sums in full.
+        bool udp_zero = false;
+        if (!STRICT) {
+            if (ip_dirty) {
+                const uint32_t hc = lds16(w, b + 10);
+                sts16(w, b + 10, ~fold32((~hc & 0xffff) + fold32(ip_diff)) & 0xffff);
+            }
+            if (l4_dirty) {
+                const uint32_t hc = lds16(w, b + 20 + fld);
+                if (proto == 17 && hc == 0) {
+                    udp_zero = true;   // recomputed in full below, after the new header is stored
+                } else {
+                    uint32_t c = ~fold32((~hc & 0xffff) + fold32(l4_diff)) & 0xffff;
+                    if (proto == 17 && c == 0) c = 0xffff;
+                    sts16(w, b + 20 + fld, c);
+                }
+            }
+        }
+        // store back: dwords covering [8, 24) when anything in the IP header or ports changed,
+        // and the dword(s) of the L4 checksum field; a dword reaching past the packet end is
+        // stored bytewise (the neighbouring bytes may belong to another packet).
+        const uint32_t* wd = (const uint32_t*)w;
+        const int lim = r0 + len;
+        auto put = [&](int j) {
+            if (4 * j + 4 <= lim) {
+                *(__attribute__((address_space(1))) uint32_t*)(arena + boff + 4 * j) = wd[j];
+            } else {
+                for (int q = 4 * j; q < lim; ++q) arena[boff + q] = w[q];
+            }
+        };
+        if (ip_dirty || l4_dirty) {
+            const int j1 = (r0 + 23) >> 2;
+            for (int j = (r0 + 8) >> 2; j <= j1; ++j) put(j);
+            if (!STRICT && l4_dirty && !udp_zero) {
+                const int f = r0 + 20 + fld;
+                for (int j = max(f >> 2, j1 + 1); j <= (f + 1) >> 2; ++j) put(j);
+            }
+        }
+        const uint8_t fl = (ip_dirty ? VPCSUM_F_IP : 0) | (l4_dirty ? VPCSUM_F_L4 : 0);
+        if (STRICT) {
             if (flags_out) flags_out[p] = fl;
             continue;
         }
-        if (ip_dirty) {
-            const uint32_t hc = ld16(l3 + 10);
-            const uint32_t s = fold32((~hc & 0xffff) + fold32(ip_diff));
-            st16(l3 + 10, ~s & 0xffff);
-        }
-        if (l4_dirty) {
-            const uint32_t hc = ld16(l4p + fld);
-            uint32_t c;
-            if (proto == 17 && hc == 0) {
-                // "no checksum" UDP: Java recomputes the full sum (UdpPacket.java:136-149)
-                const uint32_t seg = orient(lane_sum_range(l4p, l3 + len, l4p + fld), (int)((uintptr_t)l4p & 1));
-                const uint32_t ps = orient(lane_sum_range(l3 + 12, l3 + 20, nullptr), (int)((uintptr_t)l3 & 1));
-                const uint32_t l4len = (uint32_t)(len - l4o);
-                c = 0xffff - fold32(seg + ps + 17u + l4len);
-            } else {
-                const uint32_t s = fold32((~hc & 0xffff) + fold32(l4_diff));
-                c = ~s & 0xffff;
-            }
-            if (proto == 17 && c == 0) c = 0xffff;
+        if (udp_zero) {
+            // "no checksum" UDP: Java recomputes the full sum (UdpPacket.java:136-149)
+            uint8_t* l3 = arena + off;
+            uint8_t* l4p = l3 + 20;
+            const uint32_t seg = orient(lane_sum_range(l4p, l3 + len, l4p + fld), (int)((uintptr_t)l4p & 1));
+            const uint32_t ps = orient(lane_sum_range(l3 + 12, l3 + 20, nullptr), (int)((uintptr_t)l3 & 1));
+            uint32_t c = 0xffff - fold32(seg + ps + 17u + (uint32_t)(len - 20));
+            if (c == 0) c = 0xffff;
             st16(l4p + fld, c);
         }
         if (status) status[p] = VPCSUM_S_DONE;
@@ -1778,8 +1935,18 @@ hipError_t launch_nat4(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* 
     uint32_t g = (n + 255) / 256;
     uint32_t cap = (uint32_t)num_cus(dev) * 8;
     if (g > cap) g = cap;
-    hipLaunchKernelGGL(k_nat4, dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out,
-                       (int)(nat_mode & VPCSUM_NAT_STRICT_JAVA));
+    const bool strict = (nat_mode & VPCSUM_NAT_STRICT_JAVA) != 0;
+    // nat_mode bit 8 (internal tuning): force the byte-access kernel
+    const bool wide = !(nat_mode & 0x100u) && arena_len <= kMaxBufArena && !((uintptr_t)arena & 15);
+    if (wide) {
+        if (strict)
+            hipLaunchKernelGGL(k_nat4w<true>, dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out);
+        else
+            hipLaunchKernelGGL(k_nat4w<false>, dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out);
+    } else {
+        hipLaunchKernelGGL(k_nat4, dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out,
+                           strict ? 1 : 0);
+    }
     return hipGetLastError();
 }
 
