@@ -17,7 +17,8 @@ rw[:, 13:] = 0
 rw = rw.cuda()
 st = torch.zeros(n, dtype=torch.uint8, device="cuda")
 res = {"packets": n}
-for name, mode in (("rfc1624", V.NAT_RFC1624), ("strict_java", V.NAT_STRICT_JAVA)):
+for name, mode in (("rfc1624", V.NAT_RFC1624), ("strict_java", V.NAT_STRICT_JAVA),
+                   ("rfc1624_bytewise", V.NAT_RFC1624 | 0x100), ("strict_java_bytewise", V.NAT_STRICT_JAVA | 0x100)):
     for _ in range(3):
         V.nat4(arena, d, rw, n, st, mode)
     e0, e1 = V.Event(), V.Event()

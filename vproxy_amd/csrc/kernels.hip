@@ -82,14 +82,31 @@ __device__ __forceinline__ int l4_field(int proto) {
 // per-packet dirty flags to the checksum kernel through flags_override).
 constexpr int kFlagRejected = 0x80;
 
-// Default lanes per packet.  Per-packet work (descriptor decode, header masks, team reduction,
-// result write) is issued once per wave for 64/TEAM packets, so small teams amortise it;
-// the payload loop costs the same per byte for any TEAM.
+// Default lanes per packet (large tier of K2) and 16-B loads in flight per lane.  The payload
+// loop costs the same per byte for any TEAM; 8 x 6 covers a 1500-B packet in two trips.
 constexpr int kDefaultTeam = 8;
 constexpr int kDefaultUnroll = 6;
+// Small tier of the default kernel (K2): packets of at most kSmallTeam * kSmallUnroll 16-B chunks
+// (64 B incl. alignment) are streamed by 2-lane teams, 32 packets per iteration.
+constexpr int kSmallTeam = 2;
+constexpr int kSmallUnroll = 2;
 
+// Sum over the TEAM lanes of a team (aligned lane groups; every lane gets the total).  Teams of
+// up to 16 lanes reduce with DPP lane swizzles inside a row (xor 1, xor 2 by quad_perm, then
+// the half-row and row mirrors), one VALU op per step instead of an LDS-crossbar bpermute.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t v) {
+    return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
 template <int TEAM>
 __device__ __forceinline__ uint32_t team_sum(uint32_t v) {
+    if (TEAM <= 16) {
+        if (TEAM >= 2) v = dpp_add<0xB1>(v);    // quad_perm [1,0,3,2]
+        if (TEAM >= 4) v = dpp_add<0x4E>(v);    // quad_perm [2,3,0,1]
+        if (TEAM >= 8) v = dpp_add<0x141>(v);   // row_half_mirror
+        if (TEAM >= 16) v = dpp_add<0x140>(v);  // row_mirror
+        return v;
+    }
 #pragma unroll
     for (int m = TEAM / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, TEAM);
     return v;
@@ -1267,14 +1284,109 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Phase B of K2 for one tier: slots [s_begin, s_end) streamed by teams of TEAM lanes, 64/TEAM
+// packets per iteration; each team leaves {l4, ip, pseudo, stored} sums in its slot's q0.
 template <int TEAM, int U, bool VERIFY, bool NT>
-__global__ __launch_bounds__(256) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
+__device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, uint4 (*slots)[4], int lane,
+                                            int s_begin, int s_end) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    constexpr int PPI = 64 / TEAM;
+    const int tl = lane & (TEAM - 1);
+    const int tid = lane / TEAM;
+#pragma unroll 1
+    for (int base = s_begin; base < s_end; base += PPI) {
+        const int sidx = base + tid;
+        const bool act = sidx < s_end;
+        uint4* sl = slots[act ? sidx : 0];
+        uint4 a = sl[0];
+        if (!act) a = make_uint4(0, 0, 0, 0);
+        const uint32_t boff = a.x;
+        const int nch = (int)(a.y & 0xffff);
+        const int klo = (int)((a.y >> 16) & 0x3fff);
+        const uint32_t kfast = a.z;
+        const int l4hi = (int)a.w;
+        uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
+        uint32_t st_ip = 0, st_l4 = 0;
+        if (a.y >> 31) {
+            const uint4 bm = sl[1];
+            for (int rr = 0; rr * TEAM < nch; rr += U) {
+                v4u v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int k = (rr + u) * TEAM + tl;
+                    const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
+                    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int k = (rr + u) * TEAM + tl;
+                    if ((uint32_t)(k - klo) < kfast) {
+                        acc_l4 += (uint64_t)v[u].x + v[u].y;
+                        acc_l4 += (uint64_t)v[u].z + v[u].w;
+                    } else if (k >= klo) {
+                        const int c = k << 4;
+                        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
+                    } else if (u * TEAM < 4) {   // header chunks: k < klo <= 4
+                        const int hb0 = k << 3;
+                        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int hb = hb0 + 2 * j;
+                            acc_ip += w[j] & hmask((bm.x >> hb) & 3);
+                            acc_l4 += w[j] & hmask((bm.y >> hb) & 3);
+                            if (VERIFY) {
+                                st_ip += w[j] & hmask((bm.z >> hb) & 3);
+                                st_l4 += w[j] & hmask((bm.w >> hb) & 3);
+                            }
+                        }
+                    }
+                    asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
+                }
+            }
+        } else if (nch > 0) {
+            const uint4 q2 = sl[2], q3 = sl[3];
+            PktPlan pl;
+            pl.r0 = (int)q2.x; pl.l4lo = (int)q2.y; pl.fa = (int)q2.z; pl.iphi = (int)q2.w;
+            pl.iplo = (int)q3.x; pl.pslo = (int)q3.y; pl.pshi = (int)q3.z;
+            pl.l4hi = l4hi; pl.nch = nch;
+            const bool dip = (a.y >> 30) & 1;
+            for (int r = 0; r * TEAM < nch; ++r) {
+                const int k = r * TEAM + tl;
+                const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
+                const v4u vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+                const int c = k << 4;
+                const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+                if ((uint32_t)(k - klo) < kfast) {
+                    acc_l4 += (uint64_t)w[0] + w[1];
+                    acc_l4 += (uint64_t)w[2] + w[3];
+                } else if (k >= klo) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        hdr_dword(w[j], c + 4 * j, pl, dip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
+                }
+                asm volatile("" ::"v"(vv.x), "v"(vv.y), "v"(vv.z), "v"(vv.w));
+            }
+        }
+        const uint32_t s_l4 = fold32(team_sum<TEAM>(fold64(acc_l4)));
+        const uint32_t s_ip = fold32(team_sum<TEAM>(fold64(acc_ip)));
+        const uint32_t s_ps = fold32(team_sum<TEAM>(fold64(acc_ps)));
+        uint32_t s_st = 0;
+        if (VERIFY) s_st = fold32(team_sum<TEAM>(fold32(st_l4))) | (fold32(team_sum<TEAM>(fold32(st_ip))) << 16);
+        if (act && tl == 0) sl[0] = make_uint4(s_l4, s_ip, s_ps, s_st);
+    }
+}
+
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
                                                 uint8_t* __restrict__ arena_w) {
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    constexpr int PPI = 64 / TEAM;   // packets per iteration per wave
     // slot: q0 {boff, nch | klo<<16 | do_ip<<30 | fast<<31, kfast, l4hi}, q1 bitmaps,
     // q2/q3 the byte-range plan of the slow class; q0 is overwritten with the team's sums.
     __shared__ uint4 s_slot[4][64][4];
@@ -1282,8 +1394,6 @@ __global__ __launch_bounds__(256) void k_csum_d(const uint8_t* __restrict__ aren
         __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    const int tl = lane & (TEAM - 1);
-    const int tid = lane / TEAM;
     const uint32_t gw = (blockIdx.x * 256u + threadIdx.x) >> 6;
     const uint32_t wstride = gridDim.x * 4u * 64u;
 
@@ -1333,6 +1443,7 @@ __global__ __launch_bounds__(256) void k_csum_d(const uint8_t* __restrict__ aren
         }
         const int r0 = (int)(off & 15);
         int key = 0;
+        int n_small = 0;
         {
             PktPlan pl;
             pl.r0 = r0;
@@ -1372,14 +1483,19 @@ __global__ __launch_bounds__(256) void k_csum_d(const uint8_t* __restrict__ aren
                 }
             }
             const bool fastc = hbm && klo <= 4;
-            // cost class: trips of the team loop (fast class), slow class last, bad first
-            if (!bad) key = fastc ? 1 + min((pl.nch + TEAM * U - 1) / (TEAM * U), 13) : 15;
+            // cost class: bad first (key 0), then the small tier (one trip of TS x US chunks),
+            // then trips of the large tier's team loop, the slow class last
+            if (!bad) {
+                if (TS > 0 && fastc && pl.nch <= TS * US) key = 1;
+                else key = fastc ? 2 + min((pl.nch + TEAM * U - 1) / (TEAM * U), 12) : 15;
+            }
             uint32_t rank = 0, cnt = 0;
             for (int b = 0; b < 16 && cnt < 64; ++b) {
                 const uint64_t m = __ballot(key == b);
                 if (key == b)
                     rank = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
                 cnt += (uint32_t)__popcll(m);
+                if (b == 1) n_small = (int)cnt;   // keys 0 and 1 go to the small tier
             }
             key = (int)rank;   // from here on: this packet's slot
             uint4* sl = s_slot[wid][rank];
@@ -1394,88 +1510,11 @@ __global__ __launch_bounds__(256) void k_csum_d(const uint8_t* __restrict__ aren
         wave_sync_lds();
 
         // ---- phase B: teams stream the packets in slot order ----
-#pragma unroll 1
-        for (int it = 0; it < TEAM; ++it) {
-            uint4* sl = s_slot[wid][it * PPI + tid];
-            const uint4 a = sl[0];
-            const uint32_t boff = a.x;
-            const int nch = (int)(a.y & 0xffff);
-            const int klo = (int)((a.y >> 16) & 0x3fff);
-            const uint32_t kfast = a.z;
-            const int l4hi = (int)a.w;
-            uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
-            uint32_t st_ip = 0, st_l4 = 0;
-            if (a.y >> 31) {
-                const uint4 bm = sl[1];
-                for (int rr = 0; rr * TEAM < nch; rr += U) {
-                    v4u v[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const int k = (rr + u) * TEAM + tl;
-                        const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
-                        v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const int k = (rr + u) * TEAM + tl;
-                        if ((uint32_t)(k - klo) < kfast) {
-                            acc_l4 += (uint64_t)v[u].x + v[u].y;
-                            acc_l4 += (uint64_t)v[u].z + v[u].w;
-                        } else if (k >= klo) {
-                            const int c = k << 4;
-                            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
-                        } else if (u == 0) {
-                            const int hb0 = k << 3;
-                            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                const int hb = hb0 + 2 * j;
-                                acc_ip += w[j] & hmask((bm.x >> hb) & 3);
-                                acc_l4 += w[j] & hmask((bm.y >> hb) & 3);
-                                if (VERIFY) {
-                                    st_ip += w[j] & hmask((bm.z >> hb) & 3);
-                                    st_l4 += w[j] & hmask((bm.w >> hb) & 3);
-                                }
-                            }
-                        }
-                        asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
-                    }
-                }
-            } else if (nch > 0) {
-                const uint4 q2 = sl[2], q3 = sl[3];
-                PktPlan pl;
-                pl.r0 = (int)q2.x; pl.l4lo = (int)q2.y; pl.fa = (int)q2.z; pl.iphi = (int)q2.w;
-                pl.iplo = (int)q3.x; pl.pslo = (int)q3.y; pl.pshi = (int)q3.z;
-                pl.l4hi = l4hi; pl.nch = nch;
-                const bool dip = (a.y >> 30) & 1;
-                for (int r = 0; r * TEAM < nch; ++r) {
-                    const int k = r * TEAM + tl;
-                    const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
-                    const v4u vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
-                    const int c = k << 4;
-                    const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-                    if ((uint32_t)(k - klo) < kfast) {
-                        acc_l4 += (uint64_t)w[0] + w[1];
-                        acc_l4 += (uint64_t)w[2] + w[3];
-                    } else if (k >= klo) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            hdr_dword(w[j], c + 4 * j, pl, dip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
-                    }
-                    asm volatile("" ::"v"(vv.x), "v"(vv.y), "v"(vv.z), "v"(vv.w));
-                }
-            }
-            const uint32_t s_l4 = fold32(team_sum<TEAM>(fold64(acc_l4)));
-            const uint32_t s_ip = fold32(team_sum<TEAM>(fold64(acc_ip)));
-            const uint32_t s_ps = fold32(team_sum<TEAM>(fold64(acc_ps)));
-            uint32_t s_st = 0;
-            if (VERIFY) s_st = fold32(team_sum<TEAM>(fold32(st_l4))) | (fold32(team_sum<TEAM>(fold32(st_ip))) << 16);
-            if (tl == 0) sl[0] = make_uint4(s_l4, s_ip, s_ps, s_st);
+        if (TS > 0) {
+            stream_tier<(TS > 0 ? TS : 1), US, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, n_small);
+            stream_tier<TEAM, U, VERIFY, NT>(rsrc, s_slot[wid], lane, n_small, 64);
+        } else {
+            stream_tier<TEAM, U, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, 64);
         }
         wave_sync_lds();
 
@@ -1530,7 +1569,7 @@ __global__ __launch_bounds__(256) void k_csum_d(const uint8_t* __restrict__ aren
     }
 }
 
-template <int TEAM, int U>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, hipStream_t stream) {
@@ -1542,7 +1581,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_d<TEAM, U, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
+    hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
                        (const uint4*)desc, n, out, status, flags_override, arena_w)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -1637,7 +1676,19 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 43: return launch_d<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 44: return launch_d<8, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 45: return launch_d<2, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        default: return launch_c<kDefaultTeam, kDefaultUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 46: return launch_d<8, 6, 2, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 47: return launch_d<8, 6, 1, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 48: return launch_d<8, 8, 2, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 49: return launch_d<8, 6, 4, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 50: return launch_d<8, 6, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 51: return launch_d<8, 6, 2, 2, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 52: return launch_d<8, 6, 2, 2, 7>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 53: return launch_d<8, 6, 2, 2, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 54: return launch_d<8, 4, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 55: return launch_d<8, 5, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 56: return launch_d<4, 6, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 57: return launch_d<16, 3, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        default: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
     }
 #undef VPC_T
 }
