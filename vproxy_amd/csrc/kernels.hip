@@ -1381,7 +1381,7 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
     }
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -1394,28 +1394,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    const uint32_t gw = (blockIdx.x * 256u + threadIdx.x) >> 6;
+    // packet of this lane = P0 + lo.  IL = 0: a wave owns 64 consecutive packets.  IL = 1: the 4
+    // waves of a workgroup interleave in groups of 8 over 256 consecutive packets, so the teams
+    // of the whole workgroup read one contiguous 64-KB window per iteration (one DRAM stream
+    // per workgroup instead of four).
+    const uint32_t lo = IL ? (uint32_t)((lane >> 3) * 32 + wid * 8 + (lane & 7)) : (uint32_t)lane;
     const uint32_t wstride = gridDim.x * 4u * 64u;
-
-    uint32_t P0 = gw * 64u;
+    uint32_t P0 = IL ? blockIdx.x * 256u : ((blockIdx.x * 256u + threadIdx.x) >> 6) * 64u;
     uint4 dnext = make_uint4(0, 0, 0, 0);
     int fnext = 0;
-    if (P0 + lane < n) {
-        dnext = desc[P0 + lane];
-        if (flags_override) fnext = flags_override[P0 + lane];
+    if (P0 + lo < n) {
+        dnext = desc[P0 + lo];
+        if (flags_override) fnext = flags_override[P0 + lo];
     }
     for (; P0 < n; P0 += wstride) {
         // ---- phase A: this lane's packet ----
         const uint4 dv = dnext;
         const int fov = fnext;
         {
-            const uint32_t q = P0 + wstride + lane;
+            const uint32_t q = P0 + wstride + lo;
             if (q < n) {
                 dnext = desc[q];
                 if (flags_override) fnext = flags_override[q];
             }
         }
-        const bool live = P0 + lane < n;
+        const bool live = P0 + lo < n;
         const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
         const int len = dv.z & 0xffff;
         const int l4o = dv.z >> 16;
@@ -1558,18 +1561,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         if (live) {
             if (NT) {
-                if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lane));
-                if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lane));
+                if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lo));
+                if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lo));
             } else {
-                if (out) out[P0 + lane] = res_out;
-                if (status) status[P0 + lane] = (uint8_t)res_st;
+                if (out) out[P0 + lo] = res_out;
+                if (status) status[P0 + lo] = (uint8_t)res_st;
             }
         }
         wave_sync_lds();   // slots are rewritten by the next super-iteration
     }
 }
 
-template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, hipStream_t stream) {
@@ -1581,7 +1584,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
+    hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE, IL>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
                        (const uint4*)desc, n, out, status, flags_override, arena_w)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -1625,7 +1628,9 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
     if (grid <= 0) {
         int dev = 0;
         (void)hipGetDevice(&dev);
-        grid = num_cus(dev) * 8;   // 8 blocks x 4 waves = 32 waves per CU
+        // 12 workgroups per CU (2.4 waves of residency at 5 waves per SIMD): +0.5% on C2 and +4%
+        // on C3 over 8 (tools/sweep.py --bpc); C2 alone peaks at 2, where C3 loses 9%.
+        grid = num_cus(dev) * 12;
     }
     // mode bit 13 (internal tuning): plain loads instead of non-temporal ones
     const bool nt = (mode & 0x2000u) == 0;
@@ -1688,6 +1693,14 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 55: return launch_d<8, 5, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 56: return launch_d<4, 6, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 57: return launch_d<16, 3, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 58: return launch_d<8, 12, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 59: return launch_d<8, 16, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 60: return launch_d<16, 8, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 61: return launch_d<16, 12, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 62: return launch_d<8, 6, 2, 2, 1, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 63: return launch_d<8, 12, 2, 2, 1, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 64: return launch_d<8, 3, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 65: return launch_d<8, 2, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         default: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
     }
 #undef VPC_T
