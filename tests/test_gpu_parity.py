@@ -72,7 +72,7 @@ def pack(frames, infos, stride=None, pad=0):
 
 
 @pytest.mark.parametrize("pad", [0, 1, 2, 3, 14, 15, 398])
-@pytest.mark.parametrize("team", [0, 2, 3, 5, 6, 9, 12, 16, 17, 21, 22, 26, 28, 29, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 62, 63])
+@pytest.mark.parametrize("team", [0, 2, 3, 5, 6, 9, 40, 41, 43, 45, 46, 47, 48, 49, 50, 54, 58, 62])
 def test_kats_on_gpu(V, orc, pad, team):
     kats, frames, infos = kat_batch()
     arena, desc = pack(frames, infos, pad=pad)
@@ -129,7 +129,7 @@ def test_synth_matches_oracle_and_checksums(V, orc, workload, pad):
     torch.cuda.synchronize()
     assert np.array_equal(arena.cpu().numpy(), arena_o), "GPU generator differs from oracle generator"
     assert np.array_equal(V.tensor_to_desc(d), desc_o)
-    for team in (0, 2, 6, 12, 16, 21, 26, 29, 40, 41, 43, 45, 46, 47, 48, 49, 50, 62):
+    for team in (0, 2, 6, 9, 40, 41, 43, 45, 46, 47, 48, 49, 50, 62):
         out, st, written = gpu_compute(V, arena_o, desc_o, O.MODE_COMPUTE, team, write=True)
         a2 = arena_o.copy()
         oout, ost = orc.process(a2, desc_o, O.MODE_COMPUTE, write=True)
@@ -143,7 +143,7 @@ def test_synth_matches_oracle_and_checksums(V, orc, workload, pad):
     assert np.array_equal(out2, out)
 
 
-@pytest.mark.parametrize("team", [0, 27, 40, 45, 46, 47])
+@pytest.mark.parametrize("team", [0, 8, 40, 45, 46, 47])
 def test_raw_ranges(V, orc, team):
     rng = np.random.default_rng(5)
     lens = [0, 1, 2, 3, 5, 15, 16, 17, 31, 33, 63, 64, 65, 1499, 1500, 1501, 4097, 9000, 65535]
@@ -183,7 +183,7 @@ def test_bad_descriptors(V, orc, team):
     assert np.array_equal(after, arena)
 
 
-@pytest.mark.parametrize("team", [0, 27, 40, 41, 45, 46, 47, 48, 62])
+@pytest.mark.parametrize("team", [0, 8, 40, 41, 45, 46, 47, 48, 62])
 @pytest.mark.parametrize("mode", [O.MODE_COMPUTE, O.MODE_VERIFY])
 def test_mixed_batch_bad_raw_interleaved(V, orc, team, mode):
     """Rejected, raw-range and slow-class (odd offset) descriptors interleaved with ordinary
@@ -429,7 +429,7 @@ def test_full_size_c2_properties(V, orc):
         assert o[i] == w[0]
 
 
-@pytest.mark.parametrize("team", [0, 3, 9, 21, 26, 40, 45, 46, 47])
+@pytest.mark.parametrize("team", [0, 3, 9, 40, 45, 46, 47])
 def test_packet_ending_at_unaligned_arena_end(V, orc, team):
     """Arena length not a multiple of 16 and the last packet ending exactly at the arena end:
     the final partial chunk must still be read (buffer-descriptor range rounding)."""
@@ -526,3 +526,62 @@ def test_cpp_consumer_runs(V, tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "capi ok" in r.stdout
+
+
+# ---- K2 grids: grid-stride over 64-packet units at any workgroup count ----
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 4097, 40000])
+@pytest.mark.parametrize("bpc", [0, 1, 2, 5])
+def test_grids(V, orc, n, bpc):
+    """Ragged C3 batches vs oracle: partial last units, waves without a unit, 1-12 workgroups
+    per CU; repeated back to back on one stream."""
+    import torch
+    a, d = orc.synth(n, 2048, 0, O.SYNTH_C3, O.SEED, 777 + n)
+    want, want_st = orc.process(a, d)
+    arena = dev(a)
+    dt = V.desc_to_tensor(d)
+    for rep in range(2):
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        V.compute(arena, dt, n, out, st, O.MODE_COMPUTE, 0, blocks_per_cu=bpc)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want), (n, bpc, rep)
+        assert np.array_equal(st.cpu().numpy(), want_st), (n, bpc, rep)
+
+
+def test_small_grids(V, orc):
+    """Grids of 1..9 workgroups (the launcher caps the grid at ceil(m / 256) workgroups, so a
+    batch of m = 256 g packets at one workgroup per CU runs on exactly g workgroups): every
+    unit is done once and nothing past the batch is written."""
+    import torch
+    n = 64 * 53 + 17
+    a, d = orc.synth(n, 2048, 0, O.SYNTH_C3, O.SEED, 4242)
+    want, _ = orc.process(a, d)
+    arena = dev(a)
+    dt = V.desc_to_tensor(d)
+    for g in range(1, 10):
+        out = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        m = min(n, 256 * g)
+        V.compute(arena, dt, m, out, None, O.MODE_COMPUTE, 0, blocks_per_cu=1)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got[:m], want[:m]), g
+        assert np.all(got[m:] == 0xFFFFFFFF), g
+
+
+def test_two_streams_concurrent(V, orc):
+    """Launches on two streams run concurrently and share no state."""
+    import torch
+    n = 50000
+    a, d = orc.synth(n, 2048, 0, O.SYNTH_C2, O.SEED, 99)
+    want, _ = orc.process(a, d)
+    arena = dev(a)
+    dt = V.desc_to_tensor(d)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(8)]
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        V.compute(arena, dt, n, o, None, O.MODE_COMPUTE, 0, stream=(s1 if i % 2 else s2))
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), want)

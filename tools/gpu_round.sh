@@ -16,7 +16,7 @@ step() {  # name, limit, cmd...
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 400 python bench.py --steps 200 --warmup 20

@@ -55,4 +55,4 @@ for r in range(args.rounds):
 print(f"{text}: algorithmic {nbytes / n:.1f} B/pkt")
 for v in variants:
     a = np.array(res[v])
-    print(f"team=2^{v[0]} bpc={v[1] or 'def'} nt={v[2]}:  median {np.median(a):7.1f} GB/s  max {a.max():7.1f}")
+    print(f"variant={v[0]} bpc={v[1] or 'def'} nt={v[2]}:  median {np.median(a):7.1f} GB/s  max {a.max():7.1f}")

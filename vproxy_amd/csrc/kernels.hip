@@ -113,8 +113,10 @@ __device__ __forceinline__ uint32_t team_sum(uint32_t v) {
 }
 
 // ------------------------------------------------------------------------------------------
-// K1: compute / verify kernel.  One team of TEAM lanes per packet; each lane owns the
-// 16-byte chunks k = tl, tl+TEAM, ... of [align16(L3), L3+need).  U chunks per lane are
+// k_csum: team-per-packet compute / verify kernel, the fallback for arenas the buffer path
+// (K2, below) cannot address (> 4 GiB or not 16-B aligned), and the variant ids 2..11 of
+// launch_csum.  One team of TEAM lanes per packet; each lane owns the 16-byte chunks
+// k = tl, tl+TEAM, ... of [align16(L3), L3+need).  U chunks per lane are
 // loaded (global_load_dwordx4) before any is consumed so every lane keeps U*16 bytes in
 // flight; chunks fully inside the L4 payload take the 8-instruction fast path, the few
 // header / tail chunks take the byte-masked path.
@@ -306,248 +308,6 @@ __global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena,
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// K1b: "wave" form of the checksum kernel.  A wave owns 64 consecutive packets per iteration:
-//   * per-packet work is lane-parallel -- lane i decodes descriptor i (one coalesced 1 KiB
-//     load), walks packet i's header chunks (IPv4 header, pseudo addresses, L4 header, the
-//     checksum fields: the byte-masked work), and writes result i (coalesced stores);
-//   * the payload (16-B chunks from the first chunk after the L4 checksum field to the end) is
-//     streamed by teams of TEAM lanes, 64/TEAM packets at a time, fast path + one masked tail;
-//     each team's sum is handed to the packet's lane with one shuffle.
-// So the masked header work is issued once per 64 packets instead of once per 64/TEAM.
-// ------------------------------------------------------------------------------------------
-template <int TEAM, int U, int UH, bool VERIFY, bool NT>
-__global__ __launch_bounds__(256) void k_csum_wave(const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                   const uint4* __restrict__ desc, uint32_t n,
-                                                   uint32_t* __restrict__ out, uint8_t* __restrict__ status,
-                                                   const uint8_t* __restrict__ flags_override,
-                                                   uint8_t* __restrict__ arena_w) {
-    constexpr int PPS = 64 / TEAM;   // packets per payload sub-iteration
-    const int lane = threadIdx.x & 63;
-    const int tl = lane & (TEAM - 1);
-    const int tid = lane / TEAM;
-    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) >> 6;
-    const uint32_t nwaves = gridDim.x * 4u;
-
-    for (uint32_t pbase = wave * 64u; pbase < n; pbase += nwaves * 64u) {
-        const uint32_t p = pbase + lane;
-        const bool live = p < n;
-        uint4 dv = make_uint4(0, 0, 0, 0);
-        int fl = 0;
-        if (live) {
-            dv = desc[p];
-            fl = flags_override ? flags_override[p] : (int)((dv.w >> 16) & 0xff);
-        }
-        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-        const int len = dv.z & 0xffff;
-        const int l4o = dv.z >> 16;
-        const int ver = dv.w & 0xff;
-        const int proto = (dv.w >> 8) & 0xff;
-
-        bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
-        const bool raw = (fl & VPCSUM_F_RAW) != 0;
-        bool do_ip = false, do_l4 = false;
-        int fld = -1;
-        if (!bad && !raw) {
-            if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
-            else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
-            else bad = true;
-            if (!bad && (fl & VPCSUM_F_L4)) {
-                fld = l4_field(proto);
-                if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
-                else do_l4 = true;
-            }
-            if (!bad && (fl & VPCSUM_F_IP)) {
-                if (ver != 4) bad = true;
-                else do_ip = true;
-            }
-        }
-        const bool act = live && !bad;
-
-        // ---- per-packet plan (relative to the 16-B aligned base of the L3 header) ----
-        const uintptr_t l3a = (uintptr_t)(arena + off);
-        const uintptr_t basea = l3a & ~(uintptr_t)15;
-        PktPlan pl;
-        pl.r0 = (int)(l3a & 15);
-        const int need = !act ? 0 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
-        pl.nch = act ? (pl.r0 + need + 15) >> 4 : 0;
-        int fast_lo;
-        if (raw) {
-            pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
-            fast_lo = (pl.r0 + 15) & ~15;
-        } else if (do_l4) {
-            pl.l4lo = pl.r0 + l4o; pl.l4hi = pl.r0 + len; pl.fa = pl.r0 + l4o + fld;
-            fast_lo = (pl.fa + 2 + 15) & ~15;
-        } else {
-            pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
-            fast_lo = 1 << 30;
-        }
-        const int end_rel = pl.r0 + need;
-        const int H = min(fast_lo >> 4, pl.nch);   // header chunks [0, H), payload [H, nch)
-        if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
-        if (do_l4 && proto != 1) {
-            pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
-            pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
-        } else { pl.pslo = 0; pl.pshi = 0; }
-
-        // ---- header phase: one lane per packet, byte-masked ----
-        uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
-        uint32_t st_ip = 0, st_l4 = 0;
-        int hmax = H;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) hmax = max(hmax, __shfl_xor(hmax, m, 64));
-        const uint4* base = (const uint4*)basea;
-        for (int h = 0; h < hmax; h += UH) {
-            uint4 v[UH];
-#pragma unroll
-            for (int u = 0; u < UH; ++u) {
-                if (h + u < H) v[u] = ld_stream<NT>(base + h + u);
-                else v[u] = make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < UH; ++u) {
-                if (h + u >= H) continue;
-                const int c = (h + u) << 4;
-                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int d = c + 4 * j;
-                    const uint32_t mf = bmask(d, pl.fa, pl.fa + 2);
-                    acc_l4 += w[j] & bmask(d, pl.l4lo, pl.l4hi) & ~mf;
-                    const uint32_t mif = bmask(d, pl.r0 + 10, pl.r0 + 12);
-                    acc_ip += w[j] & bmask(d, pl.iplo, pl.iphi) & ~mif;
-                    acc_ps += w[j] & bmask(d, pl.pslo, pl.pshi);
-                    if (VERIFY) {
-                        st_l4 += w[j] & mf;
-                        st_ip += (w[j] & mif) & (do_ip ? 0xffffffffu : 0u);
-                    }
-                }
-            }
-        }
-
-        // ---- payload phase: TEAM lanes per packet, PPS packets at a time ----
-        const uint32_t blo = (uint32_t)basea, bhi = (uint32_t)((uint64_t)basea >> 32);
-        const int fast_hi = end_rel & ~15;
-        uint32_t my_payload = 0;
-#pragma unroll 1
-        for (int sidx = 0; sidx < TEAM; ++sidx) {
-            const int q = sidx * PPS + tid;
-            const uint32_t qlo = __shfl(blo, q, 64), qhi = __shfl(bhi, q, 64);
-            const int qH = __shfl(H, q, 64), qN = __shfl(pl.nch, q, 64);
-            const int qFH = __shfl(fast_hi, q, 64), qE = __shfl(end_rel, q, 64);
-            const uint4* qb = (const uint4*)(((uint64_t)qhi << 32) | qlo);
-            uint64_t acc = 0;
-            for (int r = 0; qH + r * TEAM < qN; r += U) {
-                uint4 v[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int k = min(qH + (r + u) * TEAM + tl, qN - 1);
-                    v[u] = ld_stream<NT>(qb + k);
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int k = qH + (r + u) * TEAM + tl;
-                    if (k >= qN) continue;
-                    const int c = k << 4;
-                    if (c + 16 <= qFH) {
-                        acc += (uint64_t)v[u].x + v[u].y;
-                        acc += (uint64_t)v[u].z + v[u].w;
-                    } else {
-                        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) acc += w[j] & tailmask(c + 4 * j, qE);
-                    }
-                }
-            }
-            const uint32_t ssum = team_sum<TEAM>(fold64(acc));
-            const uint32_t got = __shfl(ssum, (lane % PPS) * TEAM, 64);
-            if (lane / PPS == sidx) my_payload = got;
-        }
-
-        // ---- per-packet result (lane-parallel, coalesced stores) ----
-        if (!live) continue;
-        if (bad) {
-            if (out) out[p] = 0;
-            if (status) status[p] = VPCSUM_S_BAD_DESC;
-            continue;
-        }
-        uint32_t ipc = 0, l4c = 0;
-        uint8_t st = VPCSUM_S_DONE;
-        const uint32_t s_l4 = fold32(fold64(acc_l4) + my_payload);
-        if (raw) {
-            ipc = 0xffff - orient(s_l4, pl.r0);
-        } else {
-            if (do_ip) ipc = 0xffff - orient(fold64(acc_ip), pl.r0);
-            if (do_l4) {
-                uint32_t tot = orient(s_l4, pl.r0 + l4o);
-                if (proto != 1) {
-                    const uint32_t l4len = (uint32_t)(len - l4o);
-                    tot += orient(fold64(acc_ps), pl.r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
-                }
-                l4c = 0xffff - fold32(tot);
-                if (proto == 17 && l4c == 0) l4c = 0xffff;
-            }
-            if (VERIFY) {
-                if (do_ip && orient(fold32(st_ip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
-                if (do_l4) {
-                    const uint32_t stored = orient(fold32(st_l4), pl.fa);
-                    if (stored == l4c) st |= VPCSUM_S_L4_OK;
-                    if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
-                }
-            }
-            if (arena_w) {
-                uint8_t* w = arena_w + off;
-                if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
-                if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
-            }
-        }
-        if (out) out[p] = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
-        if (status) status[p] = st;
-    }
-}
-
-template <int TEAM, int U, int UH>
-static hipError_t launch_wave(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
-                              uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
-                              uint8_t* arena_w, int grid, hipStream_t stream) {
-    uint32_t need = (n + 255) / 256;   // 4 waves x 64 packets per workgroup
-    uint32_t g = grid > 0 ? (uint32_t)grid : need;
-    if (g > need) g = need;
-    if (g == 0) g = 1;
-#define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_wave<TEAM, U, UH, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,          \
-                       (const uint4*)desc, n, out, status, flags_override, arena_w)
-    if (verify) {
-        if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
-    } else {
-        if (nt) VPC_LAUNCH(false, true); else VPC_LAUNCH(false, false);
-    }
-#undef VPC_LAUNCH
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------
-// K1c: header-spread form.  One team of TEAM lanes per packet; the first 64 bytes from the
-// 16-B aligned L3 base (IPv4 header + pseudo addresses + L4 header + checksum field for every
-// ihl<=5+TCP / UDP / ICMP / IPv6-without-options packet) are split into 16/TEAM dwords per
-// lane, so the byte-masked work is 1-4 dwords per lane instead of whole chunks on a few lanes.
-// Chunks from byte 64 on are payload (8-op fast path, one masked tail); the rare headers that
-// reach past byte 64 (IPv4 options, IPv6 extension headers) take the generic masked path there.
-// All U payload loads of a lane are issued before the first is consumed.
-// ------------------------------------------------------------------------------------------
-// Header loads use the same (non-temporal) policy as the payload loads of the same 128-B line:
-// mixing a temporal and a non-temporal load on one line fetched it twice (FETCH_SIZE +30%).
-template <int HDW>
-struct HdrLoad;
-template <> struct HdrLoad<1> { typedef uint32_t T; };
-template <> struct HdrLoad<2> { typedef unsigned int T __attribute__((ext_vector_type(2))); };
-template <> struct HdrLoad<4> { typedef unsigned int T __attribute__((ext_vector_type(4))); };
-template <int HDW, bool NT>
-__device__ __forceinline__ typename HdrLoad<HDW>::T ld_hdr(uintptr_t a) {
-    typedef __attribute__((address_space(1))) const typename HdrLoad<HDW>::T GT;
-    return NT ? __builtin_nontemporal_load((GT*)a) : *(GT*)a;
-}
-
 __device__ __forceinline__ void hdr_dword(uint32_t w, int d, const PktPlan& pl, bool do_ip, uint64_t& acc_l4,
                                           uint64_t& acc_ip, uint64_t& acc_ps, uint32_t& st_l4, uint32_t& st_ip,
                                           bool verify) {
@@ -563,7 +323,8 @@ __device__ __forceinline__ void hdr_dword(uint32_t w, int d, const PktPlan& pl, 
 }
 
 // Big-endian 16-bit store of a checksum field into a frame, non-temporal (written once; a plain
-// store of a partial line costs far more beside the nt read stream -- measured 2x on k_csum_c).
+// store of a partial line costs far more beside the nt read stream -- measured 2x on an
+// earlier team-per-packet kernel).
 __device__ __forceinline__ void st_be16_nt(uint8_t* p, uint32_t v) {
     typedef __attribute__((address_space(1))) uint16_t g16;
     typedef __attribute__((address_space(1))) uint8_t g8;
@@ -584,209 +345,6 @@ __device__ __forceinline__ uint32_t hw_range(int lo, int hi) {
 __device__ __forceinline__ uint32_t hw_bit(int b) { return (b >= 0 && b < 32) ? (1u << b) : 0u; }
 // 2 halfword-select bits -> dword byte mask: bit0 -> 0x0000ffff, bit1 -> 0xffff0000
 __device__ __forceinline__ uint32_t hmask(uint32_t b) { return ((b & 1u) | ((b & 2u) << 15)) * 0xffffu; }
-
-__device__ __noinline__ void hdr_chunk_cold(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int c,
-                                            const PktPlan& pl, bool do_ip, uint64_t& acc_l4, uint64_t& acc_ip,
-                                            uint64_t& acc_ps, uint32_t& st_l4, uint32_t& st_ip, bool verify) {
-    hdr_dword(w0, c, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, verify);
-    hdr_dword(w1, c + 4, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, verify);
-    hdr_dword(w2, c + 8, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, verify);
-    hdr_dword(w3, c + 12, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, verify);
-}
-
-template <int TEAM, int U, bool VERIFY, bool NT>
-__global__ __launch_bounds__(256) void k_csum3(const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                               const uint4* __restrict__ desc, uint32_t n,
-                                               uint32_t* __restrict__ out, uint8_t* __restrict__ status,
-                                               const uint8_t* __restrict__ flags_override,
-                                               uint8_t* __restrict__ arena_w) {
-    constexpr int HDW = 16 / TEAM;   // header dwords per lane (64 B per team)
-    typedef typename HdrLoad<HDW>::T HT;
-    const int tl = threadIdx.x & (TEAM - 1);
-    const uint32_t team = (blockIdx.x * 256u + threadIdx.x) / TEAM;
-    const uint32_t nteams = gridDim.x * (256u / TEAM);
-
-    uint4 dnext = make_uint4(0, 0, 0, 0);
-    int fnext = 0;
-    if (team < n) {
-        dnext = desc[team];
-        if (flags_override) fnext = flags_override[team];
-    }
-
-    for (uint32_t p = team; p < n; p += nteams) {
-        const uint4 dv = dnext;
-        const int fov = fnext;
-        if (p + nteams < n) {
-            dnext = desc[p + nteams];
-            if (flags_override) fnext = flags_override[p + nteams];
-        }
-        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-        const int len = dv.z & 0xffff;
-        const int l4o = dv.z >> 16;
-        const int ver = dv.w & 0xff;
-        const int proto = (dv.w >> 8) & 0xff;
-        const int fl = flags_override ? fov : (int)((dv.w >> 16) & 0xff);
-
-        bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
-        const bool raw = (fl & VPCSUM_F_RAW) != 0;
-        bool do_ip = false, do_l4 = false;
-        int fld = -1;
-        if (!bad && !raw) {
-            if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
-            else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
-            else bad = true;
-            if (!bad && (fl & VPCSUM_F_L4)) {
-                fld = l4_field(proto);
-                if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
-                else do_l4 = true;
-            }
-            if (!bad && (fl & VPCSUM_F_IP)) {
-                if (ver != 4) bad = true;
-                else do_ip = true;
-            }
-        }
-        if (bad) {
-            if (tl == 0) {
-                if (out) out[p] = 0;
-                if (status) status[p] = VPCSUM_S_BAD_DESC;
-            }
-            continue;
-        }
-
-        const uint8_t* l3 = arena + off;
-        const uintptr_t basea = (uintptr_t)l3 & ~(uintptr_t)15;
-        PktPlan pl;
-        pl.r0 = (int)((uintptr_t)l3 & 15);
-        const int need = (raw || do_l4) ? len : (do_ip ? l4o : 0);
-        const int end_rel = pl.r0 + need;
-        pl.nch = (end_rel + 15) >> 4;
-        if (raw) {
-            pl.l4lo = pl.r0; pl.l4hi = end_rel; pl.fa = -64;
-            pl.fast_lo = 0;
-        } else if (do_l4) {
-            pl.l4lo = pl.r0 + l4o; pl.l4hi = end_rel; pl.fa = pl.r0 + l4o + fld;
-            pl.fast_lo = (pl.fa + 2 + 15) & ~15;
-        } else {
-            pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
-            pl.fast_lo = 1 << 30;
-        }
-        pl.fast_hi = end_rel & ~15;
-        if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
-        if (do_l4 && proto != 1) {
-            pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
-            pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
-        } else { pl.pslo = 0; pl.pshi = 0; }
-
-        uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
-        uint32_t st_ip = 0, st_l4 = 0;
-        if (end_rel > 0) {
-            // ---- issue: header dwords (64 B per team) + all payload chunks of this group ----
-            const int d0 = tl * HDW * 4;                    // first header byte of this lane
-            const int dlast = (end_rel - 1) & ~(HDW * 4 - 1);   // last in-range load of this width
-            const HT hv = ld_hdr<HDW, NT>(basea + min(d0, dlast));
-            const uint4* base = (const uint4*)basea;
-            const int npay = pl.nch - 4;                    // payload chunks [4, nch)
-            for (int r = 0; r == 0 || r * TEAM < npay; r += U) {
-                uint4 v[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int k = 4 + min((r + u) * TEAM + tl, npay - 1);
-                    if (npay > 0) v[u] = ld_stream<NT>(base + k);
-                    else v[u] = make_uint4(0, 0, 0, 0);
-                }
-                if (r == 0) {
-                    const uint32_t* hw = (const uint32_t*)&hv;
-#pragma unroll
-                    for (int j = 0; j < HDW; ++j)
-                        hdr_dword(hw[j], d0 + 4 * j, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int kk = (r + u) * TEAM + tl;
-                    if (kk >= npay) continue;
-                    const int c = (4 + kk) << 4;
-                    if (c >= pl.fast_lo && c + 16 <= pl.fast_hi) {
-                        acc_l4 += (uint64_t)v[u].x + v[u].y;
-                        acc_l4 += (uint64_t)v[u].z + v[u].w;
-                    } else if (c >= pl.fast_lo) {
-                        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
-                    } else {
-                        // long header (IPv4 options / IPv6 ext headers / IP-only): generic masks
-                        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            hdr_dword(w[j], c + 4 * j, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
-                    }
-                }
-            }
-        }
-
-        const uint32_t s_l4 = team_sum<TEAM>(fold64(acc_l4));
-        const uint32_t s_ip = team_sum<TEAM>(fold64(acc_ip));
-        const uint32_t s_ps = team_sum<TEAM>(fold64(acc_ps));
-        uint32_t s_stl4 = 0, s_stip = 0;
-        if (VERIFY) {
-            s_stl4 = team_sum<TEAM>(fold32(st_l4));
-            s_stip = team_sum<TEAM>(fold32(st_ip));
-        }
-        if (tl == 0) {
-            uint32_t ipc = 0, l4c = 0;
-            uint8_t st = VPCSUM_S_DONE;
-            if (raw) {
-                ipc = 0xffff - orient(fold32(s_l4), pl.r0);
-            } else {
-                if (do_ip) ipc = 0xffff - orient(fold32(s_ip), pl.r0);
-                if (do_l4) {
-                    uint32_t tot = orient(fold32(s_l4), pl.r0 + l4o);
-                    if (proto != 1) {
-                        const uint32_t l4len = (uint32_t)(len - l4o);
-                        tot += orient(fold32(s_ps), pl.r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
-                    }
-                    l4c = 0xffff - fold32(tot);
-                    if (proto == 17 && l4c == 0) l4c = 0xffff;
-                }
-                if (VERIFY) {
-                    if (do_ip && orient(fold32(s_stip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
-                    if (do_l4) {
-                        const uint32_t stored = orient(fold32(s_stl4), pl.fa);
-                        if (stored == l4c) st |= VPCSUM_S_L4_OK;
-                        if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
-                    }
-                }
-                if (arena_w) {
-                    uint8_t* w = arena_w + off;
-                    if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
-                    if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
-                }
-            }
-            if (out) out[p] = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
-            if (status) status[p] = st;
-        }
-    }
-}
-
-template <int TEAM, int U>
-static hipError_t launch_k3(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
-                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
-                            uint8_t* arena_w, int grid, hipStream_t stream) {
-    const uint32_t per_block = 256 / TEAM;
-    uint32_t need = (n + per_block - 1) / per_block;
-    uint32_t g = grid > 0 ? (uint32_t)grid : need;
-    if (g > need) g = need;
-    if (g == 0) g = 1;
-#define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum3<TEAM, U, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,                  \
-                       (const uint4*)desc, n, out, status, flags_override, arena_w)
-    if (verify) {
-        if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
-    } else {
-        if (nt) VPC_LAUNCH(false, true); else VPC_LAUNCH(false, false);
-    }
-#undef VPC_LAUNCH
-    return hipGetLastError();
-}
 
 template <int TEAM, int U>
 static hipError_t launch_team(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
@@ -810,13 +368,12 @@ static hipError_t launch_team(const uint8_t* arena, uint64_t arena_len, const vp
 }
 
 // ------------------------------------------------------------------------------------------
-// K1 (buffer form, the default).  Same work split as k_csum, but the packet bytes come in
-// through buffer_load_dwordx4 on ONE wave-uniform descriptor spanning the arena: a chunk past
-// the packet end gets an offset outside the descriptor's range and the hardware returns zeros
-// without touching memory.  So all U loads of a lane are issued unconditionally (no branch,
-// nothing for the compiler to sink), address math is one 32-bit add per load, and the
-// per-chunk classification is a single range test.  Needs a 16-B aligned arena < 4 GiB;
-// launch_csum falls back to k_csum otherwise.
+// Buffer addressing (K2).  The packet bytes come in through buffer_load_dwordx4 on ONE
+// wave-uniform descriptor spanning the arena: a chunk past the packet end gets an offset outside
+// the descriptor's range and the hardware returns zeros without touching memory.  So all U loads
+// of a lane are issued unconditionally (no branch, nothing for the compiler to sink), address
+// math is one 32-bit add per load, and the per-chunk classification is a single range test.
+// Needs a 16-B aligned arena < 4 GiB; launch_d falls back to k_csum otherwise.
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t kOutOfRange = 0xFFFFFF00u;
 constexpr uint64_t kMaxBufArena = 0xFFFF0000ull;
@@ -827,446 +384,6 @@ __device__ __forceinline__ uint32_t buf_records(uint64_t arena_len) {
     return (uint32_t)((arena_len + 15) & ~15ull);
 }
 
-template <int TEAM, int U, bool VERIFY, bool NT>
-__global__ __launch_bounds__(256) void k_csum_b(const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                const uint4* __restrict__ desc, uint32_t n,
-                                                uint32_t* __restrict__ out, uint8_t* __restrict__ status,
-                                                const uint8_t* __restrict__ flags_override,
-                                                uint8_t* __restrict__ arena_w) {
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
-    const int tl = threadIdx.x & (TEAM - 1);
-    const uint32_t team = (blockIdx.x * 256u + threadIdx.x) / TEAM;
-    const uint32_t nteams = gridDim.x * (256u / TEAM);
-
-    uint4 dnext = make_uint4(0, 0, 0, 0);
-    int fnext = 0;
-    if (team < n) {
-        dnext = desc[team];
-        if (flags_override) fnext = flags_override[team];
-    }
-
-    for (uint32_t p = team; p < n; p += nteams) {
-        const uint4 dv = dnext;
-        const int fov = fnext;
-        if (p + nteams < n) {   // prefetch the next descriptor while this packet streams
-            dnext = desc[p + nteams];
-            if (flags_override) fnext = flags_override[p + nteams];
-        }
-        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-        const int len = dv.z & 0xffff;
-        const int l4o = dv.z >> 16;
-        const int ver = dv.w & 0xff;
-        const int proto = (dv.w >> 8) & 0xff;
-        const int fl = flags_override ? fov : (int)((dv.w >> 16) & 0xff);
-
-        bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
-        const bool raw = (fl & VPCSUM_F_RAW) != 0;
-        bool do_ip = false, do_l4 = false;
-        int fld = -1;
-        if (!bad && !raw) {
-            if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
-            else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
-            else bad = true;
-            if (!bad && (fl & VPCSUM_F_L4)) {
-                fld = l4_field(proto);
-                if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
-                else do_l4 = true;
-            }
-            if (!bad && (fl & VPCSUM_F_IP)) {
-                if (ver != 4) bad = true;
-                else do_ip = true;
-            }
-        }
-        if (bad) {
-            if (tl == 0) {
-                if (out) out[p] = 0;
-                if (status) status[p] = VPCSUM_S_BAD_DESC;
-            }
-            continue;
-        }
-
-        PktPlan pl;
-        pl.r0 = (int)(off & 15);                          // arena is 16-B aligned
-        const uint32_t boff = (uint32_t)(off & ~(uint64_t)15);
-        const int need = (raw || do_l4) ? len : (do_ip ? l4o : 0);
-        pl.nch = (pl.r0 + need + 15) >> 4;
-        if (raw) {
-            pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
-            pl.fast_lo = (pl.r0 + 15) & ~15;
-        } else if (do_l4) {
-            pl.l4lo = pl.r0 + l4o; pl.l4hi = pl.r0 + len; pl.fa = pl.r0 + l4o + fld;
-            pl.fast_lo = (pl.fa + 2 + 15) & ~15;
-        } else {
-            pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
-            pl.fast_lo = 1 << 30;
-        }
-        pl.fast_hi = (pl.r0 + need) & ~15;
-        if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
-        if (do_l4 && proto != 1) {
-            pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
-            pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
-        } else { pl.pslo = 0; pl.pshi = 0; }
-        // chunk classes: k < klo header, klo <= k < khi payload, k >= khi tail (or past the end)
-        const int klo = min(pl.fast_lo >> 4, pl.nch);
-        const uint32_t kfast = (uint32_t)max((pl.fast_hi >> 4) - klo, 0);
-
-        uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
-        uint32_t st_ip = 0, st_l4 = 0;
-
-        for (int r0 = 0; r0 * TEAM < pl.nch; r0 += U) {
-            v4u v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int k = (r0 + u) * TEAM + tl;
-                const uint32_t bo = k < pl.nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
-                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int k = (r0 + u) * TEAM + tl;
-                if ((uint32_t)(k - klo) < kfast) {
-                    acc_l4 += (uint64_t)v[u].x + v[u].y;
-                    acc_l4 += (uint64_t)v[u].z + v[u].w;
-                } else if (k >= klo) {
-                    const int c = k << 4;
-                    const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
-                } else {
-                    const int c = k << 4;
-                    const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int d = c + 4 * j;
-                        const uint32_t mf = bmask(d, pl.fa, pl.fa + 2);
-                        acc_l4 += w[j] & bmask(d, pl.l4lo, pl.l4hi) & ~mf;
-                        const uint32_t mif = bmask(d, pl.r0 + 10, pl.r0 + 12);
-                        acc_ip += w[j] & bmask(d, pl.iplo, pl.iphi) & ~mif;
-                        acc_ps += w[j] & bmask(d, pl.pslo, pl.pshi);
-                        if (VERIFY) {
-                            st_l4 += w[j] & mf;
-                            st_ip += (w[j] & mif) & (do_ip ? 0xffffffffu : 0u);
-                        }
-                    }
-                }
-            }
-        }
-
-        const uint32_t s_l4 = team_sum<TEAM>(fold64(acc_l4));
-        const uint32_t s_ip = team_sum<TEAM>(fold64(acc_ip));
-        const uint32_t s_ps = team_sum<TEAM>(fold64(acc_ps));
-        uint32_t s_stl4 = 0, s_stip = 0;
-        if (VERIFY) {
-            s_stl4 = team_sum<TEAM>(fold32(st_l4));
-            s_stip = team_sum<TEAM>(fold32(st_ip));
-        }
-        if (tl == 0) {
-            uint32_t ipc = 0, l4c = 0;
-            uint8_t st = VPCSUM_S_DONE;
-            if (raw) {
-                ipc = 0xffff - orient(fold32(s_l4), pl.r0);
-            } else {
-                if (do_ip) ipc = 0xffff - orient(fold32(s_ip), pl.r0);
-                if (do_l4) {
-                    uint32_t tot = orient(fold32(s_l4), pl.r0 + l4o);
-                    if (proto != 1) {
-                        const uint32_t l4len = (uint32_t)(len - l4o);
-                        tot += orient(fold32(s_ps), pl.r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
-                    }
-                    l4c = 0xffff - fold32(tot);
-                    if (proto == 17 && l4c == 0) l4c = 0xffff;
-                }
-                if (VERIFY) {
-                    if (do_ip && orient(fold32(s_stip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
-                    if (do_l4) {
-                        const uint32_t stored = orient(fold32(s_stl4), pl.fa);
-                        if (stored == l4c) st |= VPCSUM_S_L4_OK;
-                        if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
-                    }
-                }
-                if (arena_w) {
-                    uint8_t* w = arena_w + off;
-                    if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
-                    if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
-                }
-            }
-            if (out) out[p] = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
-            if (status) status[p] = st;
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// K1 (buffer form with coalesced results).  As k_csum_b, but a wave owns 64 consecutive
-// packets per super-iteration (TEAM iterations of 64/TEAM packets); each team's result is
-// shuffled to lane (packet - P0) and out/status are written with one 256-B / 64-B store per
-// 64 packets instead of one 4-B / 1-B store per team (the scattered stores cost 3-4% each).
-// ------------------------------------------------------------------------------------------
-template <int TEAM, int U, bool VERIFY, bool NT, int ABL = 0, int WPE = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_c(const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                const uint4* __restrict__ desc, uint32_t n,
-                                                uint32_t* __restrict__ out, uint8_t* __restrict__ status,
-                                                const uint8_t* __restrict__ flags_override,
-                                                uint8_t* __restrict__ arena_w) {
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    constexpr int PPI = 64 / TEAM;   // packets per iteration per wave
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
-    const int lane = threadIdx.x & 63;
-    const int tl = lane & (TEAM - 1);
-    const int tid = lane / TEAM;
-    const uint32_t gw = (blockIdx.x * 256u + threadIdx.x) >> 6;
-    const uint32_t wstride = gridDim.x * 4u * 64u;
-
-    uint32_t P0 = gw * 64u;
-    uint4 dnext = make_uint4(0, 0, 0, 0);
-    int fnext = 0;
-    {
-        const uint32_t q = P0 + tid;
-        if (q < n) {
-            dnext = desc[q];
-            if (flags_override) fnext = flags_override[q];
-        }
-    }
-    for (; P0 < n; P0 += wstride) {
-        uint32_t res_out = 0, res_st = 0;
-#pragma unroll 1
-        for (int it = 0; it < TEAM; ++it) {
-            const uint32_t p = P0 + it * PPI + tid;
-            const uint4 dv = dnext;
-            const int fov = fnext;
-            {   // prefetch the descriptor of this team's next packet
-                const uint32_t q = (it + 1 < TEAM) ? p + PPI : P0 + wstride + tid;
-                if (q < n) {
-                    dnext = desc[q];
-                    if (flags_override) fnext = flags_override[q];
-                }
-            }
-            const bool live = p < n;
-            const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-            const int len = dv.z & 0xffff;
-            const int l4o = dv.z >> 16;
-            const int ver = dv.w & 0xff;
-            const int proto = (dv.w >> 8) & 0xff;
-            const int fl = flags_override ? fov : (int)((dv.w >> 16) & 0xff);
-
-            bool bad = !live || off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
-            const bool raw = (fl & VPCSUM_F_RAW) != 0;
-            bool do_ip = false, do_l4 = false;
-            int fld = -1;
-            if (!bad && !raw) {
-                if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
-                else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
-                else bad = true;
-                if (!bad && (fl & VPCSUM_F_L4)) {
-                    fld = l4_field(proto);
-                    if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
-                    else do_l4 = true;
-                }
-                if (!bad && (fl & VPCSUM_F_IP)) {
-                    if (ver != 4) bad = true;
-                    else do_ip = true;
-                }
-            }
-
-            PktPlan pl;
-            pl.r0 = (int)(off & 15);
-            const uint32_t boff = (uint32_t)(off & ~(uint64_t)15);
-            const int need = bad ? 0 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
-            pl.nch = bad ? 0 : (pl.r0 + need + 15) >> 4;
-            if (raw) {
-                pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
-                pl.fast_lo = (pl.r0 + 15) & ~15;
-            } else if (do_l4) {
-                pl.l4lo = pl.r0 + l4o; pl.l4hi = pl.r0 + len; pl.fa = pl.r0 + l4o + fld;
-                pl.fast_lo = (pl.fa + 2 + 15) & ~15;
-            } else {
-                pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
-                pl.fast_lo = 1 << 30;
-            }
-            pl.fast_hi = (pl.r0 + need) & ~15;
-            if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
-            if (do_l4 && proto != 1) {
-                pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
-                pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
-            } else { pl.pslo = 0; pl.pshi = 0; }
-            const int klo = min(pl.fast_lo >> 4, pl.nch);
-            const uint32_t kfast = (uint32_t)max((pl.fast_hi >> 4) - klo, 0);
-            // Halfword bitmaps over the first 64 B from the aligned base (even L3 start, even L4
-            // offset, no odd end inside the window): bit h selects bytes [2h, 2h+2).  B_l4 also
-            // carries the pseudo-header addresses (same orientation when l4o is even), so the
-            // common header costs ~7 ops per dword and range instead of a byte-mask chain.
-            const bool hbm = !raw && !(pl.r0 & 1) && !(l4o & 1) && ((((pl.r0 + need) & 1) == 0) || pl.r0 + need >= 64);
-            uint32_t B_ip = 0, B_l4 = 0, F_ip = 0, F_l4 = 0;
-            if (hbm) {
-                const int r0h = pl.r0 >> 1;
-                if (do_ip) {
-                    F_ip = 1u << (r0h + 5);
-                    B_ip = hw_range(r0h, r0h + (l4o >> 1)) & ~F_ip;
-                }
-                if (do_l4) {
-                    F_l4 = hw_bit(pl.fa >> 1);
-                    B_l4 = hw_range((pl.r0 + l4o) >> 1, (pl.r0 + need + 1) >> 1) & ~F_l4;
-                    if (proto != 1) B_l4 |= (ver == 4) ? hw_range(r0h + 6, r0h + 10) : hw_range(r0h + 4, r0h + 20);
-                }
-            }
-
-            uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
-            uint32_t st_ip = 0, st_l4 = 0;
-            // fast class: every header byte lies in the 64-B bitmap window.  The rare rest (odd
-            // alignment, IPv4 options / IPv6 extension headers past byte 64, raw ranges) takes a
-            // separate one-chunk-at-a-time loop, so its byte-mask temporaries never share
-            // registers with the U chunks in flight of the main loop.
-            const bool fastc = hbm && klo <= 4;
-            if (fastc) {
-                for (int r0 = 0; r0 * TEAM < pl.nch; r0 += U) {
-                    v4u v[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const int k = (r0 + u) * TEAM + tl;
-                        const uint32_t bo = k < pl.nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
-                        v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const int k = (r0 + u) * TEAM + tl;
-                        if ((ABL & 1) || (uint32_t)(k - klo) < kfast) {   // ABL&1: ablation, no masks
-                            acc_l4 += (uint64_t)v[u].x + v[u].y;
-                            acc_l4 += (uint64_t)v[u].z + v[u].w;
-                        } else if (k >= klo) {
-                            const int c = k << 4;
-                            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
-                        } else if (u == 0) {
-                            // header chunk: k < klo <= 4 <= TEAM, so only u == 0 of the first group
-                            const int hb0 = k << 3;   // halfwords [8k, 8k+8)
-                            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                const int hb = hb0 + 2 * j;
-                                acc_ip += w[j] & hmask((B_ip >> hb) & 3);
-                                acc_l4 += w[j] & hmask((B_l4 >> hb) & 3);
-                                if (VERIFY) {
-                                    st_ip += w[j] & hmask((F_ip >> hb) & 3);
-                                    st_l4 += w[j] & hmask((F_l4 >> hb) & 3);
-                                }
-                            }
-                        }
-                        // Every chunk register counts as consumed on every path.  Without this the
-                        // waitcnt pass keeps the exec-skipped loads "pending" across the back edge
-                        // and puts vmcnt(0) at the loop head, which also drains the next packet's
-                        // descriptor prefetch: one exposed memory latency per packet.
-                        asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
-                    }
-                }
-            } else {
-                for (int r = 0; r * TEAM < pl.nch; ++r) {
-                    const int k = r * TEAM + tl;
-                    const uint32_t bo = k < pl.nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
-                    const v4u vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
-                    const int c = k << 4;
-                    const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-                    if ((uint32_t)(k - klo) < kfast) {
-                        acc_l4 += (uint64_t)w[0] + w[1];
-                        acc_l4 += (uint64_t)w[2] + w[3];
-                    } else if (k >= klo) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            hdr_dword(w[j], c + 4 * j, pl, do_ip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
-                    }
-                    asm volatile("" ::"v"(vv.x), "v"(vv.y), "v"(vv.z), "v"(vv.w));
-                }
-            }
-
-            const uint32_t s_l4 = (ABL & 2) ? fold64(acc_l4) : team_sum<TEAM>(fold64(acc_l4));
-            const uint32_t s_ip = (ABL & 2) ? fold64(acc_ip) : team_sum<TEAM>(fold64(acc_ip));
-            const uint32_t s_ps = (ABL & 2) ? fold64(acc_ps) : team_sum<TEAM>(fold64(acc_ps));
-            uint32_t s_stl4 = 0, s_stip = 0;
-            if (VERIFY) {
-                s_stl4 = team_sum<TEAM>(fold32(st_l4));
-                s_stip = team_sum<TEAM>(fold32(st_ip));
-            }
-            uint32_t ro = 0, rs = VPCSUM_S_BAD_DESC;
-            if (!bad) {
-                uint32_t ipc = 0, l4c = 0;
-                uint32_t st = VPCSUM_S_DONE;
-                if (raw) {
-                    ipc = 0xffff - orient(fold32(s_l4), pl.r0);
-                } else {
-                    if (do_ip) ipc = 0xffff - orient(fold32(s_ip), pl.r0);
-                    if (do_l4) {
-                        uint32_t tot = orient(fold32(s_l4), pl.r0 + l4o);
-                        if (proto != 1) {
-                            const uint32_t l4len = (uint32_t)(len - l4o);
-                            tot += orient(fold32(s_ps), pl.r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
-                        }
-                        l4c = 0xffff - fold32(tot);
-                        if (proto == 17 && l4c == 0) l4c = 0xffff;
-                    }
-                    if (VERIFY) {
-                        if (do_ip && orient(fold32(s_stip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
-                        if (do_l4) {
-                            const uint32_t stored = orient(fold32(s_stl4), pl.fa);
-                            if (stored == l4c) st |= VPCSUM_S_L4_OK;
-                            if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
-                        }
-                    }
-                    if (arena_w && tl == 0) {
-                        uint8_t* w = arena_w + off;
-                        if (do_ip) st_be16_nt(w + 10, ipc);
-                        if (do_l4) st_be16_nt(w + l4o + fld, l4c);
-                    }
-                }
-                ro = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
-                rs = st;
-            }
-            // hand the team's result to the lane that owns packet P0 + lane
-            const int src = (lane % PPI) * TEAM;
-            const uint32_t go = __shfl(ro, src, 64);
-            const uint32_t gs = __shfl(rs, src, 64);
-            if (lane / PPI == it) { res_out = go; res_st = gs; }
-        }
-        if (P0 + lane < n) {
-            if (NT && !(ABL & 4)) {   // results are written once: stream them past the caches like the reads
-                if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lane));
-                if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lane));
-            } else {
-                if (out) out[P0 + lane] = res_out;
-                if (status) status[P0 + lane] = (uint8_t)res_st;
-            }
-        }
-    }
-}
-
-template <int TEAM, int U, int ABL = 0, int WPE = 1>
-static hipError_t launch_c(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
-                           uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
-                           uint8_t* arena_w, int grid, hipStream_t stream) {
-    if (arena_len > kMaxBufArena || ((uintptr_t)arena & 15))
-        return launch_team<TEAM, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w,
-                                    grid, stream);
-    uint32_t need = (n + 255) / 256;   // 4 waves x 64 packets per workgroup
-    uint32_t g = grid > 0 ? (uint32_t)grid : need;
-    if (g > need) g = need;
-    if (g == 0) g = 1;
-#define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_c<TEAM, U, V, N, ABL, WPE>), dim3(g), dim3(256), 0, stream, arena, arena_len,       \
-                       (const uint4*)desc, n, out, status, flags_override, arena_w)
-    if (verify) {
-        if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
-    } else {
-        if (nt) VPC_LAUNCH(false, true); else VPC_LAUNCH(false, false);
-    }
-#undef VPC_LAUNCH
-    return hipGetLastError();
-}
-
 // ------------------------------------------------------------------------------------------
 // K2: owner-lane plans, size-sorted teams.  A wave takes 64 consecutive packets per
 // super-iteration.  Lane L decodes descriptor P0+L once (validation, chunk plan, header
@@ -1274,7 +391,7 @@ static hipError_t launch_c(const uint8_t* arena, uint64_t arena_len, const vpcsu
 // `rank`.  Then TEAM iterations: team t of iteration `it` streams the packet of slot
 // it*PPI+t and leaves its partial sums in that slot.  Last, lane L reads its slot back and
 // finalizes its own packet; out/status are written coalesced.  Decode and finalize are
-// issued once per 64 packets instead of TEAM times (K1 repeats them in every team lane),
+// issued once per 64 packets instead of TEAM times (k_csum repeats them in every team lane),
 // and the sort puts packets of similar length in the same iteration, so a ragged batch
 // (C3) no longer pays the longest of PPI random packets per iteration.
 // ------------------------------------------------------------------------------------------
@@ -1282,6 +399,51 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Fast-class trips of one team over its packet's chunks [0, nch): U loads per lane issued
+// back to back, then consumed (payload fast path, masked tail, header bitmaps).
+template <int TEAM, int U, bool VERIFY, bool NT>
+__device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, uint32_t boff, int nch, int klo,
+                                           uint32_t kfast, int l4hi, const uint4 bm, int tl, uint64_t& acc_l4,
+                                           uint64_t& acc_ip, uint32_t& st_ip, uint32_t& st_l4) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    for (int rr = 0; rr * TEAM < nch; rr += U) {
+        v4u v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = (rr + u) * TEAM + tl;
+            const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = (rr + u) * TEAM + tl;
+            if ((uint32_t)(k - klo) < kfast) {
+                acc_l4 += (uint64_t)v[u].x + v[u].y;
+                acc_l4 += (uint64_t)v[u].z + v[u].w;
+            } else if (k >= klo) {
+                const int c = k << 4;
+                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
+            } else if (u * TEAM < 4) {   // header chunks: k < klo <= 4
+                const int hb0 = k << 3;
+                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int hb = hb0 + 2 * j;
+                    acc_ip += w[j] & hmask((bm.x >> hb) & 3);
+                    acc_l4 += w[j] & hmask((bm.y >> hb) & 3);
+                    if (VERIFY) {
+                        st_ip += w[j] & hmask((bm.z >> hb) & 3);
+                        st_l4 += w[j] & hmask((bm.w >> hb) & 3);
+                    }
+                }
+            }
+            asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
+        }
+    }
 }
 
 // Phase B of K2 for one tier: slots [s_begin, s_end) streamed by teams of TEAM lanes, 64/TEAM
@@ -1309,42 +471,7 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
         uint32_t st_ip = 0, st_l4 = 0;
         if (a.y >> 31) {
             const uint4 bm = sl[1];
-            for (int rr = 0; rr * TEAM < nch; rr += U) {
-                v4u v[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int k = (rr + u) * TEAM + tl;
-                    const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
-                    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int k = (rr + u) * TEAM + tl;
-                    if ((uint32_t)(k - klo) < kfast) {
-                        acc_l4 += (uint64_t)v[u].x + v[u].y;
-                        acc_l4 += (uint64_t)v[u].z + v[u].w;
-                    } else if (k >= klo) {
-                        const int c = k << 4;
-                        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
-                    } else if (u * TEAM < 4) {   // header chunks: k < klo <= 4
-                        const int hb0 = k << 3;
-                        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int hb = hb0 + 2 * j;
-                            acc_ip += w[j] & hmask((bm.x >> hb) & 3);
-                            acc_l4 += w[j] & hmask((bm.y >> hb) & 3);
-                            if (VERIFY) {
-                                st_ip += w[j] & hmask((bm.z >> hb) & 3);
-                                st_l4 += w[j] & hmask((bm.w >> hb) & 3);
-                            }
-                        }
-                    }
-                    asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
-                }
-            }
+            fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, acc_l4, acc_ip, st_ip, st_l4);
         } else if (nch > 0) {
             const uint4 q2 = sl[2], q3 = sl[3];
             PktPlan pl;
@@ -1407,13 +534,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         dnext = desc[P0 + lo];
         if (flags_override) fnext = flags_override[P0 + lo];
     }
-    for (; P0 < n; P0 += wstride) {
+    for (uint32_t Pn; P0 < n; P0 = Pn) {
         // ---- phase A: this lane's packet ----
         const uint4 dv = dnext;
         const int fov = fnext;
+        Pn = P0 + wstride;
         {
-            const uint32_t q = P0 + wstride + lo;
-            if (q < n) {
+            const uint32_t q = Pn + lo;
+            if (Pn < n && q < n) {
                 dnext = desc[q];
                 if (flags_override) fnext = flags_override[q];
             }
@@ -1572,43 +700,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// Grid of the grid-stride kernels: 12 workgroups per CU (2.4 waves of residency at 5 waves per
+// SIMD) was the best grid-stride shape across C2 / C3 (tools/sweep.py --bpc).
+static uint32_t default_grid() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return (uint32_t)num_cus(dev) * 12u;
+}
 template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, hipStream_t stream) {
     if (arena_len > kMaxBufArena || ((uintptr_t)arena & 15))
         return launch_team<TEAM, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w,
-                                    grid, stream);
+                                    grid > 0 ? grid : default_grid(), stream);
     uint32_t need = (n + 255) / 256;   // 4 waves x 64 packets per workgroup
-    uint32_t g = grid > 0 ? (uint32_t)grid : need;
+    uint32_t g = grid > 0 ? (uint32_t)grid : default_grid();
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
     hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE, IL>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
-                       (const uint4*)desc, n, out, status, flags_override, arena_w)
-    if (verify) {
-        if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
-    } else {
-        if (nt) VPC_LAUNCH(false, true); else VPC_LAUNCH(false, false);
-    }
-#undef VPC_LAUNCH
-    return hipGetLastError();
-}
-
-template <int TEAM, int U>
-static hipError_t launch_b(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
-                           uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
-                           uint8_t* arena_w, int grid, hipStream_t stream) {
-    if (arena_len > kMaxBufArena || ((uintptr_t)arena & 15))   // descriptor range / alignment
-        return launch_team<TEAM, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w,
-                                    grid, stream);
-    const uint32_t per_block = 256 / TEAM;
-    uint32_t need = (n + per_block - 1) / per_block;
-    uint32_t g = grid > 0 ? (uint32_t)grid : need;
-    if (g > need) g = need;
-    if (g == 0) g = 1;
-#define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_b<TEAM, U, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
                        (const uint4*)desc, n, out, status, flags_override, arena_w)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -1624,18 +735,12 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
                        uint8_t* arena_w, int team_log2, int grid_override, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const bool verify = (mode & VPCSUM_MODE_VERIFY) != 0;
-    int grid = grid_override;
-    if (grid <= 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        // 12 workgroups per CU (2.4 waves of residency at 5 waves per SIMD): +0.5% on C2 and +4%
-        // on C3 over 8 (tools/sweep.py --bpc); C2 alone peaks at 2, where C3 loses 9%.
-        grid = num_cus(dev) * 12;
-    }
+    const int grid = grid_override;   // <= 0: each launcher's default
     // mode bit 13 (internal tuning): plain loads instead of non-temporal ones
     const bool nt = (mode & 0x2000u) == 0;
     // variant = (lanes per packet, chunks in flight per lane); ids 2..6 are log2(lanes)
-#define VPC_T(T, U) launch_team<T, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream)
+#define VPC_T(T, U) launch_team<T, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, \
+                                      grid > 0 ? grid : (int)default_grid(), stream)
     switch (team_log2) {
         case 2: return VPC_T(4, 4);
         case 3: return VPC_T(8, 4);
@@ -1647,61 +752,20 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 9: return VPC_T(8, 12);
         case 10: return VPC_T(16, 4);
         case 11: return VPC_T(8, 8);
-        case 12: return launch_wave<8, 4, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 13: return launch_wave<8, 8, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 14: return launch_wave<16, 4, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 15: return launch_wave<4, 8, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 16: return launch_k3<8, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 17: return launch_k3<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 18: return launch_k3<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 19: return launch_k3<16, 3>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 20: return launch_k3<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 21: return launch_b<8, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 22: return launch_b<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 23: return launch_b<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 24: return launch_b<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 25: return launch_b<16, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 26: return launch_c<8, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 27: return launch_c<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 28: return launch_c<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 29: return launch_c<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        // ablation builds (wrong results; timing diagnostics only)
-        case 30: return launch_c<8, 12, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 31: return launch_c<8, 12, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 31 + 1: return launch_c<8, 12, 3>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        // occupancy targets (waves per SIMD) for the register allocator
-        case 33: return launch_c<8, 6, 0, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 34: return launch_c<8, 6, 0, 7>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 35: return launch_c<8, 6, 0, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 36: return launch_c<4, 12, 0, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 37: return launch_c<8, 6, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 40: return launch_d<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 41: return launch_d<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 42: return launch_d<4, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 43: return launch_d<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 44: return launch_d<8, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 45: return launch_d<2, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 46: return launch_d<8, 6, 2, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 47: return launch_d<8, 6, 1, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 48: return launch_d<8, 8, 2, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 49: return launch_d<8, 6, 4, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 50: return launch_d<8, 6, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 51: return launch_d<8, 6, 2, 2, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 52: return launch_d<8, 6, 2, 2, 7>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 53: return launch_d<8, 6, 2, 2, 8>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 54: return launch_d<8, 4, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 55: return launch_d<8, 5, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 56: return launch_d<4, 6, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 57: return launch_d<16, 3, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 58: return launch_d<8, 12, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 59: return launch_d<8, 16, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 60: return launch_d<16, 8, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 61: return launch_d<16, 12, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
         case 62: return launch_d<8, 6, 2, 2, 1, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 63: return launch_d<8, 12, 2, 2, 1, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 64: return launch_d<8, 3, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 65: return launch_d<8, 2, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        default: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        default: return hipErrorInvalidValue;   // unknown kernel variant id
     }
 #undef VPC_T
 }
