@@ -585,3 +585,26 @@ def test_two_streams_concurrent(V, orc):
     torch.cuda.synchronize()
     for o in outs:
         assert np.array_equal(o.cpu().numpy().view(np.uint32), want)
+
+
+def test_low_concurrency_grid(V, orc):
+    """The sampled low-concurrency grid (all 64 sampled descriptors >= 1 KiB -> 2 workgroups per
+    CU) covers every packet, including small ones the sample did not see."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = cus * 2 * 256 + 9000          # more packets than the low grid holds in one round
+    a, d = orc.synth(n, 2048, 0, O.SYNTH_C2, O.SEED, 5)
+    sampled = {(n * lane) >> 6 for lane in range(64)}
+    small = np.array([i for i in range(3, n, 7) if i not in sampled])
+    d = d.copy()
+    d["l3_len"][small] = 64            # descriptors define the range; the oracle follows them too
+    want, want_st = orc.process(a, d, O.MODE_VERIFY)
+    arena = dev(a)
+    dt = V.desc_to_tensor(d)
+    for full in (False, True):
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        V.compute(arena, dt, n, out, st, O.MODE_VERIFY, 0, full_grid=full)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want), full
+        assert np.array_equal(st.cpu().numpy(), want_st), full

@@ -131,8 +131,9 @@ int vpcsum_compute_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsu
     if (n == 0) return 0;
     if (!d_arena || !d_desc) return fail("vpcsum_compute_async: NULL arena or descriptors");
     // tuning hints (not part of the stable ABI): bits 8..12 + 24..26 kernel variant, bit 13
-    // plain (temporal) loads, bits 16..23 workgroups per CU.
-    if (mode & ~(0x07ff3fffu | VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_compute_async: bad mode 0x%x", mode);
+    // plain (temporal) loads, bit 14 no sampled low-concurrency grid, bits 16..23 workgroups
+    // per CU.
+    if (mode & ~(0x07ff7fffu | VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_compute_async: bad mode 0x%x", mode);
     uint8_t* w = (mode & VPCSUM_MODE_WRITE) ? const_cast<uint8_t*>(d_arena) : nullptr;
     int grid = 0;
     if ((mode >> 16) & 0xff) {

@@ -513,7 +513,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
-                                                uint8_t* __restrict__ arena_w) {
+                                                uint8_t* __restrict__ arena_w, uint32_t low_grid) {
     // slot: q0 {boff, nch | klo<<16 | do_ip<<30 | fast<<31, kfast, l4hi}, q1 bitmaps,
     // q2/q3 the byte-range plan of the slow class; q0 is overwritten with the team's sums.
     __shared__ uint4 s_slot[4][64][4];
@@ -526,14 +526,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // of the whole workgroup read one contiguous 64-KB window per iteration (one DRAM stream
     // per workgroup instead of four).
     const uint32_t lo = IL ? (uint32_t)((lane >> 3) * 32 + wid * 8 + (lane & 7)) : (uint32_t)lane;
-    const uint32_t wstride = gridDim.x * 4u * 64u;
+    // Concurrency by packet size (low_grid > 0).  Large uniform packets stream fastest with few
+    // packets in flight (2 workgroups per CU), small and mixed ones need the full grid to hide
+    // per-iteration latency.  Every wave reads the same 64 descriptors,
+    // spread evenly over the batch, so all waves take the same decision: when every sampled
+    // packet is >= 1 KiB the batch runs on the first low_grid workgroups only and the others
+    // leave at once.  The decision affects speed only: the grid-stride loop below covers every
+    // unit for either grid.
+    // Workgroups below low_grid work in either case and fetch their first descriptors before
+    // the sample, so the two loads overlap.
+    uint32_t grid = gridDim.x;
     uint32_t P0 = IL ? blockIdx.x * 256u : ((blockIdx.x * 256u + threadIdx.x) >> 6) * 64u;
     uint4 dnext = make_uint4(0, 0, 0, 0);
     int fnext = 0;
-    if (P0 + lo < n) {
+    const bool sample = low_grid != 0 && grid > low_grid;
+    const bool early = !sample || blockIdx.x < low_grid;
+    if (early && P0 + lo < n) {
         dnext = desc[P0 + lo];
         if (flags_override) fnext = flags_override[P0 + lo];
     }
+    if (sample) {
+        const uint4 sd = desc[(uint32_t)(((uint64_t)n * (uint32_t)lane) >> 6)];
+        if (__ballot((sd.z & 0xffffu) >= 1024u) == ~0ull) grid = low_grid;
+        if (blockIdx.x >= grid) return;   // whole workgroup, before any LDS use
+        if (!early && P0 + lo < n) {
+            dnext = desc[P0 + lo];
+            if (flags_override) fnext = flags_override[P0 + lo];
+        }
+    }
+    const uint32_t wstride = grid * 4u * 64u;
     for (uint32_t Pn; P0 < n; P0 = Pn) {
         // ---- phase A: this lane's packet ----
         const uint4 dv = dnext;
@@ -707,20 +728,32 @@ static uint32_t default_grid() {
     (void)hipGetDevice(&dev);
     return (uint32_t)num_cus(dev) * 12u;
 }
+// Low-concurrency grid of K2 for batches of large packets: 2 workgroups per CU.
+static uint32_t default_low_grid() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return (uint32_t)num_cus(dev) * 2u;
+}
+
 template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
-                           uint8_t* arena_w, int grid, hipStream_t stream) {
+                           uint8_t* arena_w, int grid, bool adapt, hipStream_t stream) {
     if (arena_len > kMaxBufArena || ((uintptr_t)arena & 15))
         return launch_team<TEAM, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w,
                                     grid > 0 ? grid : default_grid(), stream);
     uint32_t need = (n + 255) / 256;   // 4 waves x 64 packets per workgroup
     uint32_t g = grid > 0 ? (uint32_t)grid : default_grid();
+    // sampled low-concurrency grid: default grid only, not with IL (its units are per workgroup),
+    // and only when the arena is large enough to hold n packets of >= 1 KiB without overlap
+    // (otherwise the sample cannot succeed and its load latency would be pure cost)
+    const uint32_t low_grid =
+        (grid > 0 || IL != 0 || !adapt || arena_len < (uint64_t)n * 1024u) ? 0u : default_low_grid();
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
     hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE, IL>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
-                       (const uint4*)desc, n, out, status, flags_override, arena_w)
+                       (const uint4*)desc, n, out, status, flags_override, arena_w, low_grid)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
     } else {
@@ -738,6 +771,8 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
     const int grid = grid_override;   // <= 0: each launcher's default
     // mode bit 13 (internal tuning): plain loads instead of non-temporal ones
     const bool nt = (mode & 0x2000u) == 0;
+    // mode bit 14 (internal tuning): K2 without the sampled low-concurrency grid
+    const bool adapt = (mode & 0x4000u) == 0;
     // variant = (lanes per packet, chunks in flight per lane); ids 2..6 are log2(lanes)
 #define VPC_T(T, U) launch_team<T, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, \
                                       grid > 0 ? grid : (int)default_grid(), stream)
@@ -752,19 +787,19 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 9: return VPC_T(8, 12);
         case 10: return VPC_T(16, 4);
         case 11: return VPC_T(8, 8);
-        case 40: return launch_d<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 41: return launch_d<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 43: return launch_d<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 45: return launch_d<2, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 46: return launch_d<8, 6, 2, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 47: return launch_d<8, 6, 1, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 48: return launch_d<8, 8, 2, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 49: return launch_d<8, 6, 4, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 50: return launch_d<8, 6, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 54: return launch_d<8, 4, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 58: return launch_d<8, 12, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 62: return launch_d<8, 6, 2, 2, 1, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
-        case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, stream);
+        case 40: return launch_d<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 41: return launch_d<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 43: return launch_d<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 45: return launch_d<2, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 46: return launch_d<8, 6, 2, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 47: return launch_d<8, 6, 1, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 48: return launch_d<8, 8, 2, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 49: return launch_d<8, 6, 4, 4>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 50: return launch_d<8, 6, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 54: return launch_d<8, 4, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 58: return launch_d<8, 12, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 62: return launch_d<8, 6, 2, 2, 1, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         default: return hipErrorInvalidValue;   // unknown kernel variant id
     }
 #undef VPC_T

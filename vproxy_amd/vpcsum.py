@@ -135,12 +135,13 @@ def _stream(stream) -> int | None:
 # Device-resident API (torch CUDA tensors)
 # ------------------------------------------------------------------------------------------
 def compute(arena, desc, n: int | None = None, out=None, status=None, mode: int = MODE_COMPUTE,
-            team_log2: int = 0, stream=None, plain_loads: bool = False, blocks_per_cu: int = 0):
+            team_log2: int = 0, stream=None, plain_loads: bool = False, blocks_per_cu: int = 0,
+            full_grid: bool = False):
     """Checksum a device-resident batch.  `arena` uint8 tensor, `desc` tensor holding n
     16-byte vpcsum_desc_t, `out` int32/uint32 tensor (n), `status` uint8 tensor (n)."""
     if n is None:
         n = desc.numel() * desc.element_size() // 16
-    m = mode | ((team_log2 & 0x1F) << 8) | (((team_log2 >> 5) & 0x7) << 24) | (0x2000 if plain_loads else 0) | ((blocks_per_cu & 0xFF) << 16)
+    m = mode | ((team_log2 & 0x1F) << 8) | (((team_log2 >> 5) & 0x7) << 24) | (0x2000 if plain_loads else 0) | (0x4000 if full_grid else 0) | ((blocks_per_cu & 0xFF) << 16)
     _check(lib().vpcsum_compute_async(_ptr(arena), arena.numel(), _ptr(desc), n, _ptr(out), _ptr(status), m,
                                       _stream(stream)), "vpcsum_compute_async")
 
