@@ -173,6 +173,14 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena_len,
                       const vpcsum_desc_t* h_desc, uint32_t n,
                       uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket);
 int vpcsum_ctx_wait(vpcsum_ctx_t* ctx, uint64_t ticket);
+/* Low-latency flushes (idle_us > 0): submits from a registered (zero-copy) arena are handed to a
+ * small persistent grid that polls a pinned mailbox, instead of a kernel launch + event wait per
+ * batch -- the Iface.completeTx flush of a few dozen frames (XDPIface.java:227-243).  Batches
+ * then run one at a time.  The grid leaves after idle_us without a batch and is restarted by
+ * the next submit.  idle_us = 0 stops it (the default).  Other submits are unaffected. */
+int vpcsum_ctx_set_service(vpcsum_ctx_t* ctx, uint32_t idle_us);
+/* Counters of a context: batches the service ran, service grids launched (either may be NULL). */
+int vpcsum_ctx_stats(vpcsum_ctx_t* ctx, uint64_t* service_batches, uint64_t* service_launches);
 /* Pipelined host->device->host throughput helper: processes a host arena of n fixed-stride
  * frames in `chunks` double-buffered pieces over two streams (H2D || kernel || D2H). */
 int vpcsum_ctx_pipeline(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint32_t stride, uint32_t copy_bytes,
@@ -212,6 +220,8 @@ int Java_io_vproxy_vpcsum_VPCsum_registerArena(PNIEnv_vpcsum_void* env, int64_t 
  *               MemorySegment out, MemorySegment status, int mode) -> long ticket */
 int Java_io_vproxy_vpcsum_VPCsum_submit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                         void* desc, int32_t n, void* out, void* status, int32_t mode);
+/* VPCsum.setService(long ctx, int idleUs) */
+int Java_io_vproxy_vpcsum_VPCsum_setService(PNIEnv_vpcsum_void* env, int64_t ctx, int32_t idleUs);
 /* VPCsum.waitFor(long ctx, long ticket) */
 int Java_io_vproxy_vpcsum_VPCsum_waitFor(PNIEnv_vpcsum_void* env, int64_t ctx, int64_t ticket);
 /* VPCsum.close(long ctx) */

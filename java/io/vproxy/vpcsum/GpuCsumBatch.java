@@ -21,8 +21,9 @@ import java.lang.foreign.ValueLayout;
  * (SwitchUtils.checksumFlagsFor, SwitchUtils.java:297-316; XDPIface.sendPacket / completeTx,
  * XDPIface.java:100-178, 227-243): {@link #defer} records which sums of a frame are dirty instead
  * of setting VP_CSUM_* on the chunk, {@link #flush} (called at the top of Iface.completeTx, before
- * xsk.writePackets) computes every deferred sum in one GPU launch and writes the results into the
- * frames (MODE_WRITE), byte-for-byte what getRawPacket(0) would have produced
+ * xsk.writePackets) computes every deferred sum in one GPU pass (the resident service grid for
+ * flushes of up to 512 frames, a launch above that) and writes the results into the frames
+ * (MODE_WRITE), byte-for-byte what getRawPacket(0) would have produced
  * (AbstractPacket.java:15-22 -> Ipv4Packet.__updateChecksum :209-217, TcpPacket/UdpPacket/IcmpPacket
  * updateChecksumWith*).
  *
@@ -52,6 +53,8 @@ public final class GpuCsumBatch implements AutoCloseable {
         this.capacity = capacity;
         this.ctx = VPCsum.get().create(env, device, umemLen, capacity);
         VPCsum.get().registerArena(env, ctx, umem, umemLen);
+        // completeTx flushes are small: keep a resident GPU grid polling for them (20 ms idle)
+        VPCsum.get().setService(env, ctx, 20_000);
         this.desc = arena.allocate((long) DESC * capacity, 16);
         this.out = arena.allocate(4L * capacity, 16);
         this.status = arena.allocate(capacity, 16);

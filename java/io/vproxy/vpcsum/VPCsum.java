@@ -126,6 +126,27 @@ public class VPCsum {
         }
     }
 
+    private static final MethodHandle setServiceMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
+        "Java_io_vproxy_vpcsum_VPCsum_setService", long.class /* ctx */, int.class /* idleUs */);
+
+    /** Low-latency flushes: batches of up to 512 packets from a registered arena go to a resident
+     * GPU grid that polls a pinned mailbox, instead of a kernel launch each (about 13 us for 32
+     * frames instead of 19).  The grid leaves after {@code idleUs} without a batch and restarts on
+     * the next submit; 0 turns it off.  Not critical: it may wait for batches in flight. */
+    public void setService(PNIEnv ENV, long ctx, int idleUs) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) setServiceMH.invokeExact(ENV.MEMORY, ctx, idleUs);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+    }
+
     private static final MethodHandle closeMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
         "Java_io_vproxy_vpcsum_VPCsum_close", long.class /* ctx */);
 

@@ -67,6 +67,23 @@ int main() {
     memset(&envv, 0, sizeof(envv));
     CHECK(Java_io_vproxy_vpcsum_VPCsum_waitFor(&envv, h, envl.return_) == 0, "pni wait");
     CHECK(arena[14 + 10] == 0x7f && arena[14 + 11] == 0x41, "in-place IP checksum %02x%02x", arena[24], arena[25]);
+    // registered umem + low-latency service grid (what GpuCsumBatch sets up)
+    memset(&envv, 0, sizeof(envv));
+    CHECK(Java_io_vproxy_vpcsum_VPCsum_registerArena(&envv, h, arena.data(), (int64_t)arena.size()) == 0, "pni register");
+    CHECK(Java_io_vproxy_vpcsum_VPCsum_setService(&envv, h, 5000) == 0, "pni setService");
+    for (int rep = 0; rep < 3; ++rep) {
+        memset(arena.data() + 14 + 10, 0, 2);
+        memset(arena.data() + 2048 + 14 + 20 + 16, 0, 2);
+        memset(&envl, 0, sizeof(envl));
+        CHECK(Java_io_vproxy_vpcsum_VPCsum_submit(&envl, h, arena.data(), (int64_t)arena.size(), d, 2, out, st, VPCSUM_MODE_WRITE) == 0, "svc submit");
+        CHECK(Java_io_vproxy_vpcsum_VPCsum_waitFor(&envv, h, envl.return_) == 0, "svc wait");
+        CHECK(arena[24] == 0x7f && arena[25] == 0x41, "svc IP checksum %02x%02x", arena[24], arena[25]);
+        CHECK(arena[2048 + 14 + 36] == 0xf3 && arena[2048 + 14 + 37] == 0xff, "svc TCP checksum");
+    }
+    uint64_t sb = 0;
+    CHECK(vpcsum_ctx_stats((vpcsum_ctx_t*)(intptr_t)h, &sb, nullptr) == 0 && sb == 3, "service batches %llu", (unsigned long long)sb);
+    CHECK(Java_io_vproxy_vpcsum_VPCsum_setService(&envv, h, -1) == -1, "negative idle must throw");
+    CHECK(Java_io_vproxy_vpcsum_VPCsum_setService(&envv, h, 0) == 0, "pni service off");
     memset(&envl, 0, sizeof(envl));
     CHECK(Java_io_vproxy_vpcsum_VPCsum_create(&envl, 0, -1, 64) == -1, "pni bad args");
     CHECK(envl.ex.type && strcmp(envl.ex.type, "java.lang.IllegalArgumentException") == 0, "ex type");

@@ -608,3 +608,89 @@ def test_low_concurrency_grid(V, orc):
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy().view(np.uint32), want), full
         assert np.array_equal(st.cpu().numpy(), want_st), full
+
+
+# ---- low-latency service (persistent grid polling a pinned mailbox) ----
+
+def _busy_us(us):
+    import time
+    t = time.perf_counter() + us * 1e-6
+    while time.perf_counter() < t:
+        pass
+
+
+@pytest.mark.parametrize("idle_us", [5000, 40])
+def test_service_flushes(V, orc, idle_us):
+    """Flushes from a registered arena through the service: bit-exact with the oracle over
+    consecutive batches of random sizes in all three modes.  With idle_us = 40 the grid leaves
+    between most flushes, some of them while a batch is being posted; the host restarts it and
+    re-runs a batch a leaving grid did not finish."""
+    n_all, stride = 4096, 9216          # frames must not overlap: WRITE mode stores into them
+    a, d = orc.synth(n_all, stride, 14, O.SYNTH_FUZZ, O.SEED, 31 + idle_us)
+    arena = np.zeros(a.size + 4096, np.uint8)
+    arena[:a.size] = a
+    ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=n_all)
+    ctx.register(arena)
+    ctx.set_service(idle_us)
+    rng = np.random.default_rng(idle_us)
+    iters = 90
+    for it in range(iters):
+        lo = int(rng.integers(0, n_all - 1))
+        b = int(rng.integers(1, min(512, n_all - lo) + 1))     # <= the service's batch limit
+        dsc = d[lo:lo + b].copy()
+        mode = (O.MODE_COMPUTE, O.MODE_VERIFY, O.MODE_WRITE)[it % 3]
+        if it % 10 == 5:   # the host rewrites frame bytes between flushes: no stale reads
+            arena[int(dsc[0]["l3_off"]) + 30:int(dsc[0]["l3_off"]) + 60] ^= np.uint8(0x5A)
+        want_arena = arena.copy()
+        want_out, want_st = orc.process(want_arena, dsc, mode & O.MODE_VERIFY, write=bool(mode & O.MODE_WRITE))
+        out = np.zeros(b, np.uint32)
+        st = np.zeros(b, np.uint8)
+        ctx.wait(ctx.submit(arena, dsc, out, st, mode))
+        assert np.array_equal(out, want_out), it
+        assert np.array_equal(st, want_st), it
+        assert np.array_equal(arena, want_arena), it
+        _busy_us(int(rng.integers(0, 3 * idle_us)))
+    s = ctx.stats()
+    assert s["service_batches"] == iters
+    assert s["service_launches"] >= 1
+    # two flushes in flight: the second submit hands the first one's results over first
+    want_all, _ = orc.process(arena, d)
+    o1, o2 = np.zeros(300, np.uint32), np.zeros(200, np.uint32)
+    t1 = ctx.submit(arena, d[:300], o1)
+    t2 = ctx.submit(arena, d[300:500], o2)
+    ctx.wait(t2)
+    ctx.wait(t1)
+    assert np.array_equal(np.concatenate([o1, o2]), want_all[:500])
+    # a batch above the service's limit is launched as usual
+    o3 = np.zeros(n_all, np.uint32)
+    ctx.wait(ctx.submit(arena, d, o3))
+    assert np.array_equal(o3, want_all)
+    assert ctx.stats()["service_batches"] == iters + 2
+    ctx.set_service(0)
+    o4 = np.zeros(100, np.uint32)
+    ctx.wait(ctx.submit(arena, d[:100], o4))
+    assert np.array_equal(o4, want_all[:100])
+    assert ctx.stats()["service_batches"] == iters + 2
+    ctx.close()
+
+
+def test_service_egress_batch(V, orc):
+    """EgressBatch with the service: same frames as Java's full recompute after TTL rewrites."""
+    from vproxy_amd import vswitch as S
+    n, stride = 600, 2048
+    arena, desc = orc.synth(n, stride, 14, O.SYNTH_C3, O.SEED, 7)
+    orc.process(arena, desc, O.MODE_COMPUTE, write=True)
+    want = arena.copy()
+    batch = S.EgressBatch(arena, capacity=128, service_idle_us=20000)
+    for i in range(n):
+        l3 = int(desc[i]["l3_off"])
+        arena[l3 + 8] -= 1
+        want[l3 + 8] -= 1
+        one = desc[i:i + 1].copy()
+        one["flags"] = O.F_IP
+        orc.process(want, one, O.MODE_COMPUTE, write=True)
+        batch.defer(l3, int(desc[i]["l3_len"]), int(desc[i]["l4_off"]), 4, int(desc[i]["l4_proto"]), O.F_IP)
+    batch.complete_tx()
+    assert np.array_equal(arena, want)
+    assert batch.ctx.stats()["service_batches"] == batch.stats["flushes"] >= 5
+    batch.close()

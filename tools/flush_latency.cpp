@@ -1,0 +1,89 @@
+// flush_latency.cpp -- submit+wait latency of small zero-copy flushes through the C-ABI, the way
+// GpuCsumBatch.flush drives it at every Iface.completeTx (tooling; no Python in the timed loop).
+// Frames: C2-shaped IPv4/TCP 1500 B at stride 2048 in a registered arena (an AF_XDP umem
+// stand-in), MODE_WRITE.  Each size runs with a kernel launch per flush and through the
+// low-latency service grid (vpcsum_ctx_set_service).
+// Build: g++ -O2 -std=c++17 -I include tools/flush_latency.cpp -L vproxy_amd -lvpcsum
+//        -Wl,-rpath,'$ORIGIN/../vproxy_amd' -o tools/flush_latency
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
+#include "vpcsum.h"
+
+static void frame(uint8_t* l3, uint32_t i) {
+    // IPv4 (ihl 5) + TCP (doff 5) + 1460 payload bytes, deterministic content
+    memset(l3, 0, 40);
+    l3[0] = 0x45;
+    l3[2] = 1500 >> 8;
+    l3[3] = 1500 & 0xff;
+    l3[8] = 64;
+    l3[9] = 6;
+    for (int k = 0; k < 4; ++k) l3[12 + k] = (uint8_t)(i >> (8 * k)), l3[16 + k] = (uint8_t)(~i >> (8 * k));
+    l3[32] = 0x50;
+    for (int k = 40; k < 1500; ++k) l3[k] = (uint8_t)(k * 31 + i * 7);
+}
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 2000;
+    const uint32_t nmax = 8192, stride = 2048;
+    std::vector<uint8_t> arena((size_t)nmax * stride + 4096, 0);
+    std::vector<vpcsum_desc_t> desc(nmax);
+    for (uint32_t i = 0; i < nmax; ++i) {
+        frame(arena.data() + (size_t)i * stride, i);
+        memset(&desc[i], 0, sizeof(desc[i]));
+        desc[i].l3_off = (uint64_t)i * stride;
+        desc[i].l3_len = 1500;
+        desc[i].l4_off = 20;
+        desc[i].l3_ver = 4;
+        desc[i].l4_proto = 6;
+        desc[i].flags = VPCSUM_F_IP | VPCSUM_F_L4;
+    }
+    std::vector<uint32_t> out(nmax);
+    vpcsum_ctx_t* ctx = nullptr;
+    if (vpcsum_ctx_create(0, arena.size(), nmax, &ctx) || vpcsum_ctx_register_arena(ctx, arena.data(), arena.size())) {
+        fprintf(stderr, "setup: %s\n", vpcsum_last_error());
+        return 1;
+    }
+    printf("{");
+    const char* sep = "";
+    for (int svc = 0; svc < 2; ++svc) {
+        if (vpcsum_ctx_set_service(ctx, svc ? 200000 : 0)) {
+            fprintf(stderr, "service: %s\n", vpcsum_last_error());
+            return 1;
+        }
+        printf("%s\"%s\": {", sep, svc ? "service" : "launch");
+        sep = ", ";
+        const char* sep2 = "";
+        for (uint32_t b : {1u, 32u, 128u, 1024u, 8192u}) {
+            std::vector<double> us;
+            for (int it = 0; it < iters + 20; ++it) {
+                uint64_t t = 0;
+                const auto t0 = std::chrono::steady_clock::now();
+                if (vpcsum_ctx_submit(ctx, arena.data(), arena.size(), desc.data(), b, out.data(), nullptr,
+                                      VPCSUM_MODE_WRITE, &t) ||
+                    vpcsum_ctx_wait(ctx, t)) {
+                    fprintf(stderr, "flush: %s\n", vpcsum_last_error());
+                    return 1;
+                }
+                const auto t1 = std::chrono::steady_clock::now();
+                if (it >= 20) us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+            }
+            std::sort(us.begin(), us.end());
+            printf("%s\"%u\": {\"median_us\": %.1f, \"p99_us\": %.1f}", sep2, b, us[us.size() / 2],
+                   us[(size_t)(us.size() * 0.99)]);
+            sep2 = ", ";
+        }
+        printf("}");
+    }
+    uint64_t sb = 0, sl = 0;
+    vpcsum_ctx_stats(ctx, &sb, &sl);
+    printf(", \"service_batches\": %llu, \"service_launches\": %llu, \"iters\": %d}\n", (unsigned long long)sb,
+           (unsigned long long)sl, iters);
+    vpcsum_ctx_destroy(ctx);
+    return 0;
+}

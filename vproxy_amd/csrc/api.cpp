@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -73,6 +74,7 @@ struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     bool zero_copy = false;            // current batch ran on the host frames in place
+    uint32_t svc_seq = 0;              // != 0: the batch went to the low-latency service
     // the batch currently owned by this slot
     uint64_t ticket = 0;
     bool busy = false;
@@ -92,8 +94,39 @@ struct Registered {
     uint8_t* dev;    // device-side address of the page-locked mapping (zero-copy access)
 };
 
+// Zero-copy batches (frames read over PCIe) of at most this many packets run one wave per packet.
+constexpr uint32_t kZeroCopyWaveTeams = 4096;
+// Largest batch handed to the low-latency service (128 waves, one packet each per round); larger
+// ones are launched with a grid of their size, which is faster from ~1000 packets on
+// (tools/flush_latency.cpp: 1024 packets 48 us launched vs 57 us through the service).
+constexpr uint32_t kSvcBatchMax = 512;
+
+// Low-latency service of a context (kernels.hip k_csum_service).
+struct Service {
+    vpcsum::SvcMailbox* mb = nullptr;    // host-pinned, coherent (uncached on the GPU), mapped
+    vpcsum::SvcMailbox* dmb = nullptr;   // its device address
+    uint32_t* ctr = nullptr;             // device: workgroups finished with the current batch
+    hipStream_t stream = nullptr;
+    // the service's own descriptor / result buffers (pinned, coherent, mapped) and their device
+    // addresses: the same for every batch, so the parameter block rarely changes
+    vpcsum_desc_t* h_desc = nullptr;
+    uint32_t* h_out = nullptr;
+    uint8_t* h_status = nullptr;
+    vpcsum_desc_t* dh_desc = nullptr;
+    uint32_t* dh_out = nullptr;
+    uint8_t* dh_status = nullptr;
+    uint64_t par[3] = {0, 0, 0};         // arena, arena_len, arena_w last published
+    bool par_valid = false;
+    uint32_t posted = 0;                 // last batch published (seq)
+    uint64_t idle_ticks = 0;             // 100 MHz ticks
+    bool on = false;
+};
+
 struct vpcsum_ctx {
     int device = 0;
+    Service svc;
+    uint64_t svc_batches = 0;    // batches run by the service (lifetime of the context)
+    uint64_t svc_launches = 0;   // service grids launched (first start, idle restarts, re-runs)
     uint64_t max_arena = 0;
     uint32_t max_pkts = 0;
     vpcsum::Slot slots[2];
@@ -242,6 +275,65 @@ static void slot_free(Slot& s) {
     s = Slot();
 }
 
+static int slot_finish(vpcsum_ctx* c, Slot& s);
+
+static void svc_free(vpcsum_ctx* c) {
+    Service& v = c->svc;
+    if (v.mb) __atomic_store_n(&v.mb->cmd, kSvcStop, __ATOMIC_RELEASE);
+    if (v.stream) {
+        (void)hipStreamSynchronize(v.stream);   // the grid sees kSvcStop within a poll interval
+        (void)hipStreamDestroy(v.stream);
+    }
+    if (v.ctr) (void)hipFree(v.ctr);
+    if (v.mb) (void)hipHostFree(v.mb);
+    if (v.h_desc) (void)hipHostFree(v.h_desc);
+    if (v.h_out) (void)hipHostFree(v.h_out);
+    if (v.h_status) (void)hipHostFree(v.h_status);
+    c->svc = Service();
+}
+
+int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
+    if (!c) return fail("vpcsum_ctx_set_service: NULL context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    for (auto& s : c->slots)
+        if (s.busy && slot_finish(c, s) != 0) return -1;
+    svc_free(c);
+    if (idle_us == 0) return 0;
+    if (c->max_pkts > kSvcMaxPkts) return fail("vpcsum_ctx_set_service: capacity %u > %u packets", c->max_pkts, kSvcMaxPkts);
+    Service& v = c->svc;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    hipError_t e = hipSuccess;
+    if ((e = hipHostMalloc((void**)&v.mb, sizeof(SvcMailbox), fl)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&v.dmb, v.mb, 0)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&v.h_desc, (size_t)c->max_pkts * sizeof(vpcsum_desc_t), fl)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&v.h_out, (size_t)c->max_pkts * 4, fl)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&v.h_status, (size_t)c->max_pkts, fl)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&v.dh_desc, v.h_desc, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&v.dh_out, v.h_out, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&v.dh_status, v.h_status, 0)) != hipSuccess ||
+        (e = hipMalloc((void**)&v.ctr, sizeof(uint32_t))) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking)) != hipSuccess) {
+        svc_free(c);
+        return hipfail(e, "vpcsum_ctx_set_service allocation");
+    }
+    memset((void*)v.mb, 0, sizeof(SvcMailbox));
+    v.mb->desc = (uint64_t)(uintptr_t)v.dh_desc;
+    v.mb->out = (uint64_t)(uintptr_t)v.dh_out;
+    v.mb->status = (uint64_t)(uintptr_t)v.dh_status;
+    v.idle_ticks = (uint64_t)idle_us * 100u;   // s_memrealtime runs at 100 MHz
+    v.on = true;
+    return 0;
+}
+
+int vpcsum_ctx_stats(vpcsum_ctx_t* c, uint64_t* service_batches, uint64_t* service_launches) {
+    if (!c) return fail("vpcsum_ctx_stats: NULL context");
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (service_batches) *service_batches = c->svc_batches;
+    if (service_launches) *service_launches = c->svc_launches;
+    return 0;
+}
+
 int vpcsum_ctx_create(int device, uint64_t max_arena_bytes, uint32_t max_pkts, vpcsum_ctx_t** out) {
     if (!out) return fail("vpcsum_ctx_create: out is NULL");
     if (max_arena_bytes == 0 || max_pkts == 0) return fail("vpcsum_ctx_create: zero capacity");
@@ -256,9 +348,9 @@ int vpcsum_ctx_create(int device, uint64_t max_arena_bytes, uint32_t max_pkts, v
             (e = hipMalloc((void**)&s.d_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t))) != hipSuccess ||
             (e = hipMalloc((void**)&s.d_out, (size_t)max_pkts * 4)) != hipSuccess ||
             (e = hipMalloc((void**)&s.d_status, (size_t)max_pkts)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t), hipHostMallocMapped)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_out, (size_t)max_pkts * 4, hipHostMallocMapped)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_status, (size_t)max_pkts, hipHostMallocMapped)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_out, (size_t)max_pkts * 4, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_status, (size_t)max_pkts, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&s.dh_desc, s.h_desc, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&s.dh_out, s.h_out, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&s.dh_status, s.h_status, 0)) != hipSuccess ||
@@ -277,6 +369,7 @@ int vpcsum_ctx_create(int device, uint64_t max_arena_bytes, uint32_t max_pkts, v
 int vpcsum_ctx_destroy(vpcsum_ctx_t* c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
+    svc_free(c);
     for (auto& s : c->slots) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
         slot_free(s);
@@ -333,11 +426,47 @@ static bool is_registered(vpcsum_ctx* c, const uint8_t* p, uint64_t len) {
     return false;
 }
 
+static uint32_t svc_done(const Service& v) { return __atomic_load_n(&v.mb->done, __ATOMIC_ACQUIRE); }
+
+// (Re)start the service grid: it treats batches after `seen` as new.  Only called while no grid
+// of this context runs (stream idle), so the finished-wave counter can be cleared first.
+static int svc_launch(vpcsum_ctx* c, uint32_t seen) {
+    Service& v = c->svc;
+    VPC_CHECK(hipMemsetAsync(v.ctr, 0, sizeof(uint32_t), v.stream), "service counter reset");
+    VPC_CHECK(launch_service(v.dmb, v.ctr, seen, v.idle_ticks, v.stream), "service launch");
+    ++c->svc_launches;
+    return 0;
+}
+
+// Wait until the service has completed batch `seq`.  A grid that left on its idle timeout while
+// the batch was being posted may have done part of it: once the stream is idle the batch is run
+// again from the start by a fresh grid (the sums do not read the fields they write).
+static int svc_wait(vpcsum_ctx* c, uint32_t seq) {
+    Service& v = c->svc;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 1; (int32_t)(svc_done(v) - seq) < 0; ++spin) {
+        __builtin_ia32_pause();
+        if ((spin & 255) != 0) continue;
+        if (hipStreamQuery(v.stream) == hipSuccess && (int32_t)(svc_done(v) - seq) < 0) {
+            if (svc_launch(c, seq - 1) != 0) return -1;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+            return fail("vpcsum service: batch %u not completed within 10 s", seq);
+    }
+    return 0;
+}
+
 static int slot_finish(vpcsum_ctx* c, Slot& s) {
     if (!s.busy) return 0;
-    VPC_CHECK(hipEventSynchronize(s.done), "hipEventSynchronize");
-    if (s.user_out) memcpy(s.user_out, s.h_out, (size_t)s.n * 4);
-    if (s.user_status) memcpy(s.user_status, s.h_status, s.n);
+    if (s.svc_seq) {
+        if (svc_wait(c, s.svc_seq) != 0) return -1;
+    } else {
+        VPC_CHECK(hipEventSynchronize(s.done), "hipEventSynchronize");
+    }
+    const uint32_t* res_out = s.svc_seq ? c->svc.h_out : s.h_out;
+    const uint8_t* res_status = s.svc_seq ? c->svc.h_status : s.h_status;
+    if (s.user_out) memcpy(s.user_out, res_out, (size_t)s.n * 4);
+    if (s.user_status) memcpy(s.user_status, res_status, s.n);
     if ((s.mode & VPCSUM_MODE_WRITE) && s.user_arena && !s.zero_copy) {
         // place the GPU results into the caller's frames (big endian, as ByteArray.int16)
         for (uint32_t i = 0; i < s.n; ++i) {
@@ -354,6 +483,7 @@ static int slot_finish(vpcsum_ctx* c, Slot& s) {
         }
     }
     s.busy = false;
+    s.svc_seq = 0;
     return 0;
 }
 
@@ -389,10 +519,52 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
         // kernel reads them over PCIe in place, takes the descriptors from and writes the
         // results to pinned staging, and with MODE_WRITE stores the checksum fields straight
         // into the frames -- no DMA copy in either direction.
-        memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
         uint8_t* base = dev_arena - lo;   // device address of h_arena[0]
+        Service& v = c->svc;
+        if (v.on && n <= kSvcBatchMax) {
+            // low-latency service: one batch at a time; descriptors into the service's buffer,
+            // the parameter block if it changed, then the command word
+            for (auto& o : c->slots)   // the previous service batch: done, results handed over
+                if (o.busy && o.svc_seq && slot_finish(c, o) != 0) return -1;
+            SvcMailbox* mb = v.mb;
+            memcpy(v.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
+            const uint64_t par[3] = {(uint64_t)(uintptr_t)base, arena_len,
+                                     (mode & VPCSUM_MODE_WRITE) ? (uint64_t)(uintptr_t)base : 0};
+            uint64_t cmd = 0;
+            if (!v.par_valid || memcmp(par, v.par, sizeof(par)) != 0) {
+                mb->arena = par[0];
+                mb->arena_len = par[1];
+                mb->arena_w = par[2];
+                memcpy(v.par, par, sizeof(par));
+                v.par_valid = true;
+                cmd |= kSvcParams;
+            }
+            const uint32_t seq = v.posted + 1 ? v.posted + 1 : 1;
+            cmd |= seq | ((uint64_t)n << 32) | ((mode & VPCSUM_MODE_VERIFY) ? kSvcVerify : 0);
+            __atomic_store_n(&mb->cmd, cmd, __ATOMIC_RELEASE);
+            v.posted = seq;
+            ++c->svc_batches;
+            if (hipStreamQuery(v.stream) == hipSuccess && svc_launch(c, seq - 1) != 0) return -1;
+            s.zero_copy = true;
+            s.svc_seq = seq;
+            s.busy = true;
+            s.ticket = t;
+            s.n = n;
+            s.mode = mode;
+            s.user_arena = h_arena;
+            s.user_desc = h_desc;
+            s.user_out = h_out;
+            s.user_status = h_status;
+            *ticket = t;
+            return 0;
+        }
+        memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
+        // up to kZeroCopyWaveTeams packets: one wave per packet (variant 6, 64 lanes x 4 loads),
+        // so the batch is a few PCIe round trips deep instead of K2's per-unit iterations
+        const int variant = n <= kZeroCopyWaveTeams ? 6 : 0;
         VPC_CHECK(launch_csum(base, arena_len, s.dh_desc, n, s.dh_out, s.dh_status, nullptr,
-                              mode & VPCSUM_MODE_VERIFY, (mode & VPCSUM_MODE_WRITE) ? base : nullptr, 0, 0, s.stream),
+                              mode & VPCSUM_MODE_VERIFY, (mode & VPCSUM_MODE_WRITE) ? base : nullptr, variant, 0,
+                              s.stream),
                   "checksum launch (zero-copy)");
         s.zero_copy = true;
     } else {
@@ -552,6 +724,15 @@ int Java_io_vproxy_vpcsum_VPCsum_submit(PNIEnv_vpcsum_long* env, int64_t ctx, vo
 
 int Java_io_vproxy_vpcsum_VPCsum_waitFor(PNIEnv_vpcsum_void* env, int64_t ctx, int64_t ticket) {
     if (vpcsum_ctx_wait((vpcsum_ctx_t*)(intptr_t)ctx, (uint64_t)ticket) != 0) return pni_throw(env, "java.io.IOException");
+    return 0;
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_setService(PNIEnv_vpcsum_void* env, int64_t ctx, int32_t idleUs) {
+    if (idleUs < 0) {
+        fail("setService: negative idle time %d", idleUs);
+        return pni_throw(env, "java.lang.IllegalArgumentException");
+    }
+    if (vpcsum_ctx_set_service((vpcsum_ctx_t*)(intptr_t)ctx, (uint32_t)idleUs) != 0) return pni_throw(env, "java.io.IOException");
     return 0;
 }
 

@@ -12,6 +12,21 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
                        uint32_t* out, uint8_t* status, const uint8_t* flags_override, uint32_t mode,
                        uint8_t* arena_w, int team_log2, int grid_override, hipStream_t stream);
 
+// Low-latency service (k_csum_service): a small persistent grid that polls this host-pinned,
+// device-mapped, uncached mailbox instead of being launched per batch.  The host writes the
+// batch's descriptors into the service's own pinned buffers, the parameter block when it
+// changed, then the command word; the grid writes `done` = seq when the batch is finished.
+struct alignas(64) SvcMailbox {
+    uint64_t cmd;        // host: seq (bits 0..31, 0 = none yet) | n (32..59) | kSvcStop | kSvcVerify | kSvcParams
+    uint64_t arena, arena_len, arena_w, desc, out, status, rsv;   // device addresses; read when kSvcParams
+    alignas(64) uint32_t done;   // device: last completed batch
+};
+static_assert(sizeof(uint64_t) * 8 == 64, "SvcMailbox parameter block: one 64-B line");
+constexpr uint64_t kSvcStop = 1ull << 61, kSvcVerify = 1ull << 62, kSvcParams = 1ull << 63;
+constexpr uint32_t kSvcMaxPkts = (1u << 28) - 1;
+constexpr int kServiceGrid = 32;   // workgroups: 4 waves each, one packet per wave and round
+hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream);
+
 hipError_t launch_nat4(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const vpcsum_nat4_t* rw,
                        uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream);
 

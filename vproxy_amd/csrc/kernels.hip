@@ -131,15 +131,17 @@ struct PktPlan {
     int pslo, pshi;         // pseudo-header address bytes (rel); empty if none
 };
 
+// Body for workgroup `blk` of a grid of `gdim` workgroups (k_csum: the launch grid;
+// k_csum_service: the persistent service grid, once per batch).
 template <int TEAM, int U, bool VERIFY, bool NT>
-__global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                              const uint4* __restrict__ desc, uint32_t n,
-                                              uint32_t* __restrict__ out, uint8_t* __restrict__ status,
-                                              const uint8_t* __restrict__ flags_override,
-                                              uint8_t* __restrict__ arena_w) {
+__device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                       const uint4* __restrict__ desc, uint32_t n,
+                                       uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                       const uint8_t* __restrict__ flags_override,
+                                       uint8_t* __restrict__ arena_w, uint32_t blk, uint32_t gdim) {
     const int tl = threadIdx.x & (TEAM - 1);
-    const uint32_t team = (blockIdx.x * 256u + threadIdx.x) / TEAM;
-    const uint32_t nteams = gridDim.x * (256u / TEAM);
+    const uint32_t team = (blk * 256u + threadIdx.x) / TEAM;
+    const uint32_t nteams = gdim * (256u / TEAM);
 
     uint4 dnext = make_uint4(0, 0, 0, 0);
     int fnext = 0;
@@ -346,6 +348,15 @@ __device__ __forceinline__ uint32_t hw_bit(int b) { return (b >= 0 && b < 32) ? 
 // 2 halfword-select bits -> dword byte mask: bit0 -> 0x0000ffff, bit1 -> 0xffff0000
 __device__ __forceinline__ uint32_t hmask(uint32_t b) { return ((b & 1u) | ((b & 2u) << 15)) * 0xffffu; }
 
+template <int TEAM, int U, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                              const uint4* __restrict__ desc, uint32_t n,
+                                              uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                              const uint8_t* __restrict__ flags_override,
+                                              uint8_t* __restrict__ arena_w) {
+    k1_run<TEAM, U, VERIFY, NT>(arena, arena_len, desc, n, out, status, flags_override, arena_w, blockIdx.x, gridDim.x);
+}
+
 template <int TEAM, int U>
 static hipError_t launch_team(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                               uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
@@ -508,12 +519,14 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
     }
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                const uint4* __restrict__ desc, uint32_t n,
-                                                uint32_t* __restrict__ out, uint8_t* __restrict__ status,
-                                                const uint8_t* __restrict__ flags_override,
-                                                uint8_t* __restrict__ arena_w, uint32_t low_grid) {
+// K2 body for workgroup `blk` of a grid of `gdim` workgroups (k_csum_d: the launch grid;
+// k_csum_service: the persistent service grid, once per batch).
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL>
+__device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                       const uint4* __restrict__ desc, uint32_t n,
+                                       uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                       const uint8_t* __restrict__ flags_override,
+                                       uint8_t* __restrict__ arena_w, uint32_t low_grid, uint32_t blk, uint32_t gdim) {
     // slot: q0 {boff, nch | klo<<16 | do_ip<<30 | fast<<31, kfast, l4hi}, q1 bitmaps,
     // q2/q3 the byte-range plan of the slow class; q0 is overwritten with the team's sums.
     __shared__ uint4 s_slot[4][64][4];
@@ -535,12 +548,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // unit for either grid.
     // Workgroups below low_grid work in either case and fetch their first descriptors before
     // the sample, so the two loads overlap.
-    uint32_t grid = gridDim.x;
-    uint32_t P0 = IL ? blockIdx.x * 256u : ((blockIdx.x * 256u + threadIdx.x) >> 6) * 64u;
+    uint32_t grid = gdim;
+    uint32_t P0 = IL ? blk * 256u : ((blk * 256u + threadIdx.x) >> 6) * 64u;
     uint4 dnext = make_uint4(0, 0, 0, 0);
     int fnext = 0;
     const bool sample = low_grid != 0 && grid > low_grid;
-    const bool early = !sample || blockIdx.x < low_grid;
+    const bool early = !sample || blk < low_grid;
     if (early && P0 + lo < n) {
         dnext = desc[P0 + lo];
         if (flags_override) fnext = flags_override[P0 + lo];
@@ -548,7 +561,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (sample) {
         const uint4 sd = desc[(uint32_t)(((uint64_t)n * (uint32_t)lane) >> 6)];
         if (__ballot((sd.z & 0xffffu) >= 1024u) == ~0ull) grid = low_grid;
-        if (blockIdx.x >= grid) return;   // whole workgroup, before any LDS use
+        if (blk >= grid) return;   // whole workgroup, before any LDS use
         if (!early && P0 + lo < n) {
             dnext = desc[P0 + lo];
             if (flags_override) fnext = flags_override[P0 + lo];
@@ -719,6 +732,105 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         wave_sync_lds();   // slots are rewritten by the next super-iteration
     }
+}
+
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                const uint4* __restrict__ desc, uint32_t n,
+                                                uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                                const uint8_t* __restrict__ flags_override,
+                                                uint8_t* __restrict__ arena_w, uint32_t low_grid) {
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL>(arena, arena_len, desc, n, out, status, flags_override, arena_w, low_grid,
+                                            blockIdx.x, gridDim.x);
+}
+
+// ------------------------------------------------------------------------------------------
+// Low-latency service: the checksum on a persistent grid of kServiceGrid workgroups that polls
+// a host mailbox (internal.h SvcMailbox) instead of being launched per batch, for the small
+// flushes of Iface.completeTx (XDPIface.java:227-243) on a registered umem, where a kernel
+// launch plus an event wait cost more than the work.  Thread 0 of each workgroup polls the
+// command word at system scope; a new batch is processed by all workgroups (one packet per
+// wave, grid-stride); each workgroup releases its results at system scope and bumps a device
+// counter, and the workgroup that completes the count resets it and publishes `done`.  The grid
+// leaves on kSvcStop or after idle_ticks (100 MHz s_memrealtime) without a batch; the host
+// relaunches it on demand and re-runs a batch that a leaving grid left unfinished (idempotent:
+// checksum fields are excluded from the sums they hold).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* __restrict__ ctr, uint32_t seen,
+                                                      uint64_t idle_ticks) {
+    // batch parameters, read over PCIe by thread 0 when the host flags them as changed and kept
+    // in LDS across batches: arena, arena_len, arena_w, desc, out, status
+    __shared__ uint64_t s_par[6];
+    __shared__ uint64_t s_cmd;
+    bool have_par = false;
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (threadIdx.x == 0) {
+            uint64_t cmd = 0;
+            for (;;) {   // one 8-B PCIe read per poll
+                const uint64_t w = __hip_atomic_load(&mb->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (w & kSvcStop) break;
+                if ((uint32_t)w != seen) { cmd = w; break; }
+                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            // acquire at system scope: the frames, descriptors and parameters the host wrote
+            // before the command word are read fresh (no kernel boundary invalidates caches here)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            if (cmd && ((cmd & kSvcParams) || !have_par)) {
+                // the 64-B block in one round trip: four independent 16-B loads
+                typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+                const v4u* pb = (const v4u*)mb;
+                v4u q[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) q[k] = __builtin_nontemporal_load(pb + k);
+                s_par[0] = (uint64_t)q[0].z | ((uint64_t)q[0].w << 32);   // arena
+                s_par[1] = (uint64_t)q[1].x | ((uint64_t)q[1].y << 32);   // arena_len
+                s_par[2] = (uint64_t)q[1].z | ((uint64_t)q[1].w << 32);   // arena_w
+                s_par[3] = (uint64_t)q[2].x | ((uint64_t)q[2].y << 32);   // desc
+                s_par[4] = (uint64_t)q[2].z | ((uint64_t)q[2].w << 32);   // out
+                s_par[5] = (uint64_t)q[3].x | ((uint64_t)q[3].y << 32);   // status
+            }
+            s_cmd = cmd;
+        }
+        __syncthreads();
+        const uint64_t cmd = s_cmd;
+        const uint8_t* arena = (const uint8_t*)s_par[0];
+        const uint64_t alen = s_par[1];
+        uint8_t* arena_w = (uint8_t*)s_par[2];
+        const uint4* desc = (const uint4*)s_par[3];
+        uint32_t* out = (uint32_t*)s_par[4];
+        uint8_t* status = (uint8_t*)s_par[5];
+        __syncthreads();   // s_cmd / s_par are rewritten next round
+        if (cmd == 0) return;
+        have_par = true;
+        const uint32_t n = (uint32_t)(cmd >> 32) & kSvcMaxPkts;
+        // one wave per packet: a small flush is a few PCIe round trips deep (descriptor, frame
+        // bytes, results) instead of K2's per-unit iterations, which a latency of ~3 us per
+        // round trip would serialize
+        if (cmd & kSvcVerify)
+            k1_run<64, 4, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+        else
+            k1_run<64, 4, false, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+        // the workgroup's stores are complete (barrier); thread 0 releases them system-wide and
+        // counts the workgroup; the last workgroup of the grid publishes `done`
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            const uint32_t d = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (d + 1 == gridDim.x) {
+                __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&mb->done, (uint32_t)cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        seen = (uint32_t)cmd;
+        t0 = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream) {
+    hipLaunchKernelGGL(k_csum_service, dim3(kServiceGrid), dim3(256), 0, stream, d_mb, d_ctr, seen, idle_ticks);
+    return hipGetLastError();
 }
 
 // Grid of the grid-stride kernels: 12 workgroups per CU (2.4 waves of residency at 5 waves per

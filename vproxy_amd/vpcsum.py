@@ -35,10 +35,10 @@ EXPORTS = [
     "vpcsum_synth_async", "vpcsum_event_create", "vpcsum_event_destroy", "vpcsum_event_record",
     "vpcsum_event_elapsed_ms", "vpcsum_stream_sync", "vpcsum_ctx_create", "vpcsum_ctx_destroy",
     "vpcsum_ctx_register_arena", "vpcsum_ctx_unregister_arena", "vpcsum_ctx_submit", "vpcsum_ctx_wait",
-    "vpcsum_ctx_pipeline",
+    "vpcsum_ctx_pipeline", "vpcsum_ctx_set_service", "vpcsum_ctx_stats",
     "Java_io_vproxy_vpcsum_VPCsum_create", "Java_io_vproxy_vpcsum_VPCsum_registerArena",
     "Java_io_vproxy_vpcsum_VPCsum_submit", "Java_io_vproxy_vpcsum_VPCsum_waitFor",
-    "Java_io_vproxy_vpcsum_VPCsum_close",
+    "Java_io_vproxy_vpcsum_VPCsum_close", "Java_io_vproxy_vpcsum_VPCsum_setService",
 ]
 
 
@@ -75,6 +75,8 @@ def _declare(L):
         "vpcsum_ctx_destroy": ([P], I),
         "vpcsum_ctx_register_arena": ([P, P, U64], I),
         "vpcsum_ctx_unregister_arena": ([P, P], I),
+        "vpcsum_ctx_set_service": ([P, U32], I),
+        "vpcsum_ctx_stats": ([P, P, P], I),
         "vpcsum_ctx_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
         "vpcsum_ctx_wait": ([P, U64], I),
         "vpcsum_ctx_pipeline": ([P, P, U32, U32, P, U32, P, U32, U32], I),
@@ -216,6 +218,15 @@ class Context:
 
     def wait(self, ticket: int):
         _check(lib().vpcsum_ctx_wait(self.h, ticket), "vpcsum_ctx_wait")
+
+    def set_service(self, idle_us: int):
+        """Low-latency flushes from registered arenas (persistent service grid); 0 = off."""
+        _check(lib().vpcsum_ctx_set_service(self.h, idle_us), "vpcsum_ctx_set_service")
+
+    def stats(self) -> dict:
+        b, n = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().vpcsum_ctx_stats(self.h, ctypes.byref(b), ctypes.byref(n)), "vpcsum_ctx_stats")
+        return {"service_batches": b.value, "service_launches": n.value}
 
     def run(self, arena, desc, mode: int = MODE_COMPUTE):
         out = np.zeros(len(desc), np.uint32)

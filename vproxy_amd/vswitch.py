@@ -36,14 +36,20 @@ class EgressBatch:
 
     ``defer`` is O(1) host work (fills a 16-B descriptor); ``complete_tx`` submits the batch and
     waits: one GPU launch per flush, results written in place (MODE_WRITE).  With
-    ``register=True`` the arena is page-locked once and the kernel works on it zero-copy."""
+    ``register=True`` the arena is page-locked once and the kernel works on it zero-copy; with
+    ``service_idle_us`` > 0 as well, flushes go to the low-latency service grid
+    (vpcsum_ctx_set_service) instead of a kernel launch each."""
 
-    def __init__(self, arena: np.ndarray, capacity: int = 4096, device: int = 0, register: bool = True):
+    def __init__(self, arena: np.ndarray, capacity: int = 4096, device: int = 0, register: bool = True,
+                 service_idle_us: int = 0):
         self.arena = arena
         self.capacity = capacity
         self.ctx = V.Context(device, max_arena=max(arena.nbytes, 1 << 16), max_pkts=capacity)
         if register:
             self.ctx.register(arena)
+            if service_idle_us:
+                # flushes go to the persistent service grid instead of a launch each
+                self.ctx.set_service(service_idle_us)
         self.desc = np.zeros(capacity, V.DESC_DTYPE)
         self.out = np.zeros(capacity, np.uint32)
         self.status = np.zeros(capacity, np.uint8)
