@@ -22,5 +22,5 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 400 python bench.py --steps 200 --warmup 20
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
-  step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline
+  step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline
 fi

@@ -20,6 +20,7 @@ ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--mode", type=int, default=0)
 ap.add_argument("--noout", type=int, default=0)
+ap.add_argument("--full", default="0", help="1 = no sampled low-concurrency grid (K2 tuning bit 14)")
 args = ap.parse_args()
 
 sid, n, stride, text = WORKLOADS[args.workload]
@@ -30,18 +31,19 @@ torch.cuda.synchronize()
 nbytes = algorithmic_bytes(V.tensor_to_desc(d))
 ref = torch.zeros(n, dtype=torch.int32, device="cuda")
 V.compute(arena, d, n, ref, None, 0, 4)
-variants = [(t, b, nt) for t in map(int, args.teams.split(",")) for b in map(int, args.bpc.split(","))
-            for nt in map(int, args.nt.split(","))]
+variants = [(t, b, nt, f) for t in map(int, args.teams.split(",")) for b in map(int, args.bpc.split(","))
+            for nt in map(int, args.nt.split(",")) for f in map(int, args.full.split(","))]
 res = {v: [] for v in variants}
 out = torch.zeros(n, dtype=torch.int32, device="cuda")
 st = torch.zeros(n, dtype=torch.uint8, device="cuda")
 e0, e1 = V.Event(), V.Event()
 for r in range(args.rounds):
     for v in variants:
-        t, b, nt = v
+        t, b, nt, f = v
         o_ = None if args.noout in (1, 3) else out
         s_ = None if args.noout in (1, 2) else st
-        run = lambda: V.compute(arena, d, n, o_, s_, args.mode, t, plain_loads=not nt, blocks_per_cu=b)
+        run = lambda: V.compute(arena, d, n, o_, s_, args.mode, t, plain_loads=not nt, blocks_per_cu=b,
+                                 full_grid=bool(f))
         for _ in range(3):
             run()
         e0.record()
@@ -55,4 +57,4 @@ for r in range(args.rounds):
 print(f"{text}: algorithmic {nbytes / n:.1f} B/pkt")
 for v in variants:
     a = np.array(res[v])
-    print(f"variant={v[0]} bpc={v[1] or 'def'} nt={v[2]}:  median {np.median(a):7.1f} GB/s  max {a.max():7.1f}")
+    print(f"variant={v[0]} bpc={v[1] or 'def'} nt={v[2]} full={v[3]}:  median {np.median(a):7.1f} GB/s  max {a.max():7.1f}")
