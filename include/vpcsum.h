@@ -143,6 +143,7 @@ int vpcsum_read_probe_async(const uint8_t* d_buf, uint64_t bytes, uint32_t* d_si
 #define VPCSUM_SYNTH_C3_MIXED     3  /* IPv4 {64,576,1500} x {UDP,TCP,ICMP}  */
 #define VPCSUM_SYNTH_C4_V6JUMBO   4  /* IPv6/TCP L3 9000 B                   */
 #define VPCSUM_SYNTH_FUZZ         5  /* v4/v6, options, odd lengths, all protos */
+#define VPCSUM_SYNTH_C5_NAT1500   6  /* IPv4 L3 1500 B, TCP or UDP (50/50): NAT input */
 int vpcsum_synth_async(uint8_t* d_arena, uint64_t arena_len, uint32_t n, uint32_t stride,
                        uint32_t l3_pad, uint32_t workload, uint64_t seed, uint64_t first_index,
                        vpcsum_desc_t* d_desc, void* stream);

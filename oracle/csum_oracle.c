@@ -330,6 +330,7 @@ static orc_shape orc_shape_of(uint32_t workload, uint64_t seed, uint64_t pkt) {
             break;
         }
         case VPCSUM_SYNTH_C4_V6JUMBO: s.ver = 6; s.proto = 6; s.l3_len = 9000; s.l4_off = 40; break;
+        case VPCSUM_SYNTH_C5_NAT1500: s.proto = (r & 1) ? 17 : 6; break;
         default: { /* FUZZ */
             static const uint32_t protos4[4] = {6, 17, 1, 6};
             static const uint32_t protos6[4] = {6, 17, 58, 17};

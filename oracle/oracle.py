@@ -277,5 +277,5 @@ class Oracle:
         return int(self.L.orc_rng(seed, pkt, word))
 
 
-SYNTH_C1, SYNTH_C2, SYNTH_C3, SYNTH_C4, SYNTH_FUZZ = 1, 2, 3, 4, 5
+SYNTH_C1, SYNTH_C2, SYNTH_C3, SYNTH_C4, SYNTH_FUZZ, SYNTH_C5 = 1, 2, 3, 4, 5, 6
 SEED = 0x20241020

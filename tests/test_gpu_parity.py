@@ -115,7 +115,7 @@ def test_pcap_verify_on_gpu(V, orc):
     assert int(np.sum(st & O.S_L4_OK > 0)) == 19   # 12 CHECKSUM_PARTIAL host-TX frames fail
 
 
-@pytest.mark.parametrize("workload", [O.SYNTH_C1, O.SYNTH_C2, O.SYNTH_C3, O.SYNTH_C4, O.SYNTH_FUZZ])
+@pytest.mark.parametrize("workload", [O.SYNTH_C1, O.SYNTH_C2, O.SYNTH_C3, O.SYNTH_C4, O.SYNTH_FUZZ, O.SYNTH_C5])
 @pytest.mark.parametrize("pad", [0, 1, 14, 398])
 def test_synth_matches_oracle_and_checksums(V, orc, workload, pad):
     import torch
@@ -228,7 +228,7 @@ def _nat_batch(orc, n, seed=3, corrupt=0.0, udp_zero=0.0, pad=0, workload=O.SYNT
         arena = np.concatenate(parts)
         desc = desc.copy()
         desc["l3_off"] = offs
-    if workload != O.SYNTH_C3:
+    if workload not in (O.SYNTH_C3, O.SYNTH_C5):
         udp_zero = 0.0
     rw = np.zeros(n, O.NAT4_DTYPE)
     rw["src"] = rng.integers(0, 256, (n, 4))
@@ -249,7 +249,7 @@ def _nat_batch(orc, n, seed=3, corrupt=0.0, udp_zero=0.0, pad=0, workload=O.SYNT
 
 
 @pytest.mark.parametrize("pad", [0, 1, 2, 14, 15])
-@pytest.mark.parametrize("workload", [O.SYNTH_C1, O.SYNTH_C3, O.SYNTH_FUZZ])
+@pytest.mark.parametrize("workload", [O.SYNTH_C1, O.SYNTH_C3, O.SYNTH_FUZZ, O.SYNTH_C5])
 @pytest.mark.parametrize("packed", [False, True])
 def test_nat_wide_and_scalar_kernels(V, orc, pad, workload, packed):
     """Both NAT kernels (wide LDS-staged and byte-access, nat_mode bit 8) against the Java

@@ -7,8 +7,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000 // 8
 stride = 2048
 arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
 d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
-V.synth(arena, n, stride, 0, V.SYNTH_C3, 0x20241020, 0, d)
-# C5: 1500 B TCP/UDP with valid checksums -> use C2 lengths but alternate TCP/UDP via the C3 mix
+V.synth(arena, n, stride, 0, V.SYNTH_C5, 0x20241020, 0, d)
+# C5: 1500 B IPv4 TCP/UDP (50/50) with valid input checksums, every packet rewritten
 V.compute(arena, d, n, None, None, V.MODE_WRITE)
 g = torch.Generator(device="cpu").manual_seed(5)
 rw = torch.randint(0, 256, (n, 16), dtype=torch.uint8, generator=g)

@@ -221,7 +221,7 @@ int vpcsum_synth_async(uint8_t* d_arena, uint64_t arena_len, uint32_t n, uint32_
                        uint32_t workload, uint64_t seed, uint64_t first_index, vpcsum_desc_t* d_desc, void* stream) {
     if (n == 0) return 0;
     if (!d_arena) return fail("vpcsum_synth_async: NULL arena");
-    if (workload < VPCSUM_SYNTH_C1_UDP64 || workload > VPCSUM_SYNTH_FUZZ) return fail("vpcsum_synth_async: bad workload %u", workload);
+    if (workload < VPCSUM_SYNTH_C1_UDP64 || workload > VPCSUM_SYNTH_C5_NAT1500) return fail("vpcsum_synth_async: bad workload %u", workload);
     const uint32_t maxlen = (workload == VPCSUM_SYNTH_C4_V6JUMBO || workload == VPCSUM_SYNTH_FUZZ) ? 9000
                             : (workload == VPCSUM_SYNTH_C1_UDP64) ? 50 : 1500;
     if ((uint64_t)l3_pad + maxlen > stride) return fail("vpcsum_synth_async: stride %u < l3_pad %u + %u", stride, l3_pad, maxlen);

@@ -21,7 +21,7 @@ S_IP_OK, S_L4_OK, S_UDP_NOCSUM, S_DONE, S_BAD_DESC = 0x01, 0x02, 0x04, 0x40, 0x8
 MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
 NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL = 0x01, 0x02, 0x04, 0x08, 0x10
 NAT_RFC1624, NAT_STRICT_JAVA = 0x00, 0x01
-SYNTH_C1, SYNTH_C2, SYNTH_C3, SYNTH_C4, SYNTH_FUZZ = 1, 2, 3, 4, 5
+SYNTH_C1, SYNTH_C2, SYNTH_C3, SYNTH_C4, SYNTH_FUZZ, SYNTH_C5 = 1, 2, 3, 4, 5, 6
 
 DESC_DTYPE = np.dtype([("l3_off", "<u8"), ("l3_len", "<u2"), ("l4_off", "<u2"), ("l3_ver", "u1"),
                        ("l4_proto", "u1"), ("flags", "u1"), ("rsv", "u1")])
