@@ -258,7 +258,8 @@ def test_nat_wide_and_scalar_kernels(V, orc, pad, workload, packed):
     arena, desc, rw = _nat_batch(orc, n, seed=pad + 17, udp_zero=0.1, pad=pad, workload=workload, packed=packed)
     want = arena.copy()
     orc.nat4_java(want, desc, rw)
-    for force_scalar in (0, 0x100):
+    # default, byte-access kernel (bit 8), wide kernel with 1 / 2 / 4 packets per lane (bits 12..14)
+    for force_scalar in (0, 0x100, 0x1000, 0x2000, 0x3000):
         got, st = _gpu_nat(V, arena, desc, rw, V.NAT_RFC1624 | force_scalar)
         v4 = desc["l3_ver"] == 4
         assert np.all(st[v4] == O.S_DONE) and np.all(st[~v4] == O.S_BAD_DESC)

@@ -3,7 +3,7 @@ import json, os, sys, time
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vproxy_amd import vpcsum as V  # noqa: E402
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000 // 8
+n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 10_000_000 // 8
 stride = 2048
 arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
 d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
@@ -17,8 +17,11 @@ rw[:, 13:] = 0
 rw = rw.cuda()
 st = torch.zeros(n, dtype=torch.uint8, device="cuda")
 res = {"packets": n}
-for name, mode in (("rfc1624", V.NAT_RFC1624), ("strict_java", V.NAT_STRICT_JAVA),
-                   ("rfc1624_bytewise", V.NAT_RFC1624 | 0x100), ("strict_java_bytewise", V.NAT_STRICT_JAVA | 0x100)):
+modes = [("rfc1624", V.NAT_RFC1624), ("strict_java", V.NAT_STRICT_JAVA),
+         ("rfc1624_bytewise", V.NAT_RFC1624 | 0x100), ("strict_java_bytewise", V.NAT_STRICT_JAVA | 0x100)]
+if "--sweep" in sys.argv:   # packets per lane of the wide kernel (nat_mode bits 12..14)
+    modes += [(f"rfc1624_w{1 << k}", V.NAT_RFC1624 | ((k + 1) << 12)) for k in range(3)]
+for name, mode in modes:
     for _ in range(3):
         V.nat4(arena, d, rw, n, st, mode)
     e0, e1 = V.Event(), V.Event()

@@ -43,19 +43,21 @@ def main(tag):
             json.dump(d, open(os.path.join(P, f"{tag}_{out}.json"), "w"), indent=1)
     for src in sorted(glob.glob(os.path.join(G, "pmc_*"))):
         wl = os.path.basename(src)[4:]
+        kern = "k_nat4w" if wl == "nat" else "k_csum"
         dst = os.path.join(P, f"{tag}_pmc_{wl}")
         os.makedirs(dst, exist_ok=True)
         for f in sorted(glob.glob(os.path.join(src, "p*_counter_collection.csv"))):
             i = os.path.basename(f).split("_")[0][1:]
             rows = list(csv.DictReader(open(f)))
-            keep = [r for r in rows if "k_csum" in r["Kernel_Name"]]
+            keep = [r for r in rows if kern in r["Kernel_Name"]]
             if not keep:
                 continue
-            with open(os.path.join(dst, f"pass{i}_k_csum.csv"), "w", newline="") as fo:
+            with open(os.path.join(dst, f"pass{i}_{kern}.csv"), "w", newline="") as fo:
                 w = csv.DictWriter(fo, fieldnames=list(keep[0].keys()))
                 w.writeheader()
                 w.writerows(keep)
-        subprocess.check_call([sys.executable, os.path.join(REPO, "tools", "traffic.py"), dst], stdout=subprocess.DEVNULL)
+        subprocess.check_call([sys.executable, os.path.join(REPO, "tools", "traffic.py"), dst, kern],
+                              stdout=subprocess.DEVNULL)
     print("saved", sorted(f for f in os.listdir(P) if f.startswith(tag)))
 
 

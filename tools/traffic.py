@@ -3,14 +3,14 @@
 Correction per MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE (= TCC_EA0_RDREQ x 64 B, in KiB)
 reports exactly half of the bytes of a wide coalesced streaming read (128-B requests tallied at
 64 B), so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE (KiB) is exact for 16-B-per-lane
-stores and is taken as is.  Usage: python tools/traffic.py profiles/r01_pmc_c2 [kernel-substring]
+stores and is taken as is.  Usage: python tools/traffic.py profiles/r01_pmc_c2 [kernel-substring (default k_csum)]
 """
 import csv, glob, json, sys, collections
 d = sys.argv[1]
 ks = sys.argv[2] if len(sys.argv) > 2 else "k_csum"
 vals = collections.defaultdict(list)
 name = None
-for f in sorted(glob.glob(f"{d}/pass*_k_csum.csv")):
+for f in sorted(glob.glob(f"{d}/pass*.csv")):
     for r in csv.DictReader(open(f)):
         if ks in r["Kernel_Name"]:
             name = r["Kernel_Name"].split("(")[0]

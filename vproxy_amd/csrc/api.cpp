@@ -184,7 +184,9 @@ int vpcsum_nat4_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t*
                       uint32_t n, uint8_t* d_status, uint32_t nat_mode, void* stream) {
     if (n == 0) return 0;
     if (!d_arena || !d_desc || !d_rw) return fail("vpcsum_nat4_async: NULL arena, descriptors or rewrite table");
-    if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u)) return fail("vpcsum_nat4_async: bad nat_mode 0x%x", nat_mode);
+    // tuning hints (not part of the stable ABI): bit 8 byte-access kernel, bits 12..14 packets
+    // per lane of the wide kernel
+    if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u | 0x7000u)) return fail("vpcsum_nat4_async: bad nat_mode 0x%x", nat_mode);
     hipStream_t s = (hipStream_t)stream;
     if (nat_mode & VPCSUM_NAT_STRICT_JAVA) {
         if (!d_status) return fail("vpcsum_nat4_async: strict-java mode needs a status buffer");

@@ -1058,7 +1058,142 @@ __global__ __launch_bounds__(256) void k_nat4(uint8_t* __restrict__ arena, uint6
 __device__ __forceinline__ uint32_t lds16(const uint8_t* w, int q) { return ((uint32_t)w[q] << 8) | w[q + 1]; }
 __device__ __forceinline__ void sts16(uint8_t* w, int q, uint32_t v) { w[q] = (uint8_t)(v >> 8); w[q + 1] = (uint8_t)v; }
 
+// One packet of the wide form, after its window arrived: stage in this lane's LDS slot `w`,
+// rewrite, store back.  `wide` false: the packet takes the byte-access path instead.
 template <bool STRICT>
+__device__ __forceinline__ void nat4w_apply(uint8_t* __restrict__ arena, uint64_t arena_len,
+                                            const vpcsum_desc_t* __restrict__ desc,
+                                            const vpcsum_nat4_t* __restrict__ rw, uint32_t p, const uint4 dv,
+                                            const uint4 rv, bool wide, const uint4* v, uint8_t* w,
+                                            uint2 (*slot)[9], uint8_t* __restrict__ status,
+                                            uint8_t* __restrict__ flags_out) {
+    if (!wide) {
+        nat4_scalar(arena, arena_len, desc[p], rw[p], p, status, flags_out, STRICT ? 1 : 0);
+        return;
+    }
+    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+    const int len = dv.z & 0xffff;
+    const int proto = (dv.w >> 8) & 0xff;
+    const int mask = rv.w & 0xff;
+    const int fld = (proto == 6 || proto == 17) ? l4_field(proto) : -1;
+    const bool l4 = fld >= 0 && len - 20 >= fld + 2;
+    const int r0 = (int)(off & 15);
+    const uint32_t boff = (uint32_t)(off - (uint64_t)r0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        (*slot)[2 * k] = make_uint2(v[k].x, v[k].y);
+        (*slot)[2 * k + 1] = make_uint2(v[k].z, v[k].w);
+    }
+    const int b = r0;   // packet byte 0 inside the window
+    uint32_t ip_diff = 0, l4_diff = 0;
+    bool ip_dirty = false, l4_dirty = false;
+    if (mask & VPCSUM_NAT_SRC) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint32_t m = lds16(w, b + 12 + 2 * i);
+            const uint32_t mn = (((rv.x >> (16 * i)) & 0xff) << 8) | ((rv.x >> (16 * i + 8)) & 0xff);
+            ip_diff += (~m & 0xffff) + mn;
+            l4_diff += (~m & 0xffff) + mn;
+            sts16(w, b + 12 + 2 * i, mn);
+        }
+        ip_dirty = true; l4_dirty = true;
+    }
+    if (mask & VPCSUM_NAT_DST) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint32_t m = lds16(w, b + 16 + 2 * i);
+            const uint32_t mn = (((rv.y >> (16 * i)) & 0xff) << 8) | ((rv.y >> (16 * i + 8)) & 0xff);
+            ip_diff += (~m & 0xffff) + mn;
+            l4_diff += (~m & 0xffff) + mn;
+            sts16(w, b + 16 + 2 * i, mn);
+        }
+        ip_dirty = true; l4_dirty = true;
+    }
+    if (mask & VPCSUM_NAT_DEC_TTL) {
+        const uint32_t m = lds16(w, b + 8);
+        const uint32_t mn = (((m >> 8) - 1) & 0xff) << 8 | (m & 0xff);
+        ip_diff += (~m & 0xffff) + mn;
+        sts16(w, b + 8, mn);
+        ip_dirty = true;
+    }
+    if (l4) {
+        if (mask & VPCSUM_NAT_SPORT) {
+            const uint32_t m = lds16(w, b + 20);
+            const uint32_t mn = ((rv.z & 0xff) << 8) | ((rv.z >> 8) & 0xff);
+            l4_diff += (~m & 0xffff) + mn;
+            sts16(w, b + 20, mn);
+            l4_dirty = true;
+        }
+        if (mask & VPCSUM_NAT_DPORT) {
+            const uint32_t m = lds16(w, b + 22);
+            const uint32_t mn = (((rv.z >> 16) & 0xff) << 8) | ((rv.z >> 24) & 0xff);
+            l4_diff += (~m & 0xffff) + mn;
+            sts16(w, b + 22, mn);
+            l4_dirty = true;
+        }
+    } else {
+        l4_dirty = false;
+    }
+    bool udp_zero = false;
+    if (!STRICT) {
+        if (ip_dirty) {
+            const uint32_t hc = lds16(w, b + 10);
+            sts16(w, b + 10, ~fold32((~hc & 0xffff) + fold32(ip_diff)) & 0xffff);
+        }
+        if (l4_dirty) {
+            const uint32_t hc = lds16(w, b + 20 + fld);
+            if (proto == 17 && hc == 0) {
+                udp_zero = true;   // recomputed in full below, after the new header is stored
+            } else {
+                uint32_t c = ~fold32((~hc & 0xffff) + fold32(l4_diff)) & 0xffff;
+                if (proto == 17 && c == 0) c = 0xffff;
+                sts16(w, b + 20 + fld, c);
+            }
+        }
+    }
+    // store back: dwords covering [8, 24) when anything in the IP header or ports changed,
+    // and the dword(s) of the L4 checksum field; a dword reaching past the packet end is
+    // stored bytewise (the neighbouring bytes may belong to another packet).
+    const uint32_t* wd = (const uint32_t*)w;
+    const int lim = r0 + len;
+    auto put = [&](int j) {
+        if (4 * j + 4 <= lim) {
+            *(__attribute__((address_space(1))) uint32_t*)(arena + boff + 4 * j) = wd[j];
+        } else {
+            for (int q = 4 * j; q < lim; ++q) arena[boff + q] = w[q];
+        }
+    };
+    if (ip_dirty || l4_dirty) {
+        const int j1 = (r0 + 23) >> 2;
+        for (int j = (r0 + 8) >> 2; j <= j1; ++j) put(j);
+        if (!STRICT && l4_dirty && !udp_zero) {
+            const int f = r0 + 20 + fld;
+            for (int j = max(f >> 2, j1 + 1); j <= (f + 1) >> 2; ++j) put(j);
+        }
+    }
+    const uint8_t fl = (ip_dirty ? VPCSUM_F_IP : 0) | (l4_dirty ? VPCSUM_F_L4 : 0);
+    if (STRICT) {
+        if (flags_out) flags_out[p] = fl;
+        return;
+    }
+    if (udp_zero) {
+        // "no checksum" UDP: Java recomputes the full sum (UdpPacket.java:136-149)
+        uint8_t* l3 = arena + off;
+        uint8_t* l4p = l3 + 20;
+        const uint32_t seg = orient(lane_sum_range(l4p, l3 + len, l4p + fld), (int)((uintptr_t)l4p & 1));
+        const uint32_t ps = orient(lane_sum_range(l3 + 12, l3 + 20, nullptr), (int)((uintptr_t)l3 & 1));
+        uint32_t c = 0xffff - fold32(seg + ps + 17u + (uint32_t)(len - 20));
+        if (c == 0) c = 0xffff;
+        st16(l4p + fld, c);
+    }
+    if (status) status[p] = VPCSUM_S_DONE;
+}
+
+// W packets per lane and iteration (p, p + T, ..., T = lanes of the grid): all their
+// descriptor / rewrite loads, then all their window loads are issued before the first packet
+// is rewritten, so a lane keeps W header windows in flight instead of one (the kernel is
+// latency-bound: ~4 dependent memory steps per packet).  The LDS slot is reused per packet.
+template <bool STRICT, int W>
 __global__ __launch_bounds__(256) void k_nat4w(uint8_t* __restrict__ arena, uint64_t arena_len,
                                               const vpcsum_desc_t* __restrict__ desc,
                                               const vpcsum_nat4_t* __restrict__ rw, uint32_t n,
@@ -1069,155 +1204,71 @@ __global__ __launch_bounds__(256) void k_nat4w(uint8_t* __restrict__ arena, uint
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
     uint8_t* w = (uint8_t*)&s_win[threadIdx.x][0];
-    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
-        const uint4 dv = ((const uint4*)desc)[p];
-        const uint4 rv = ((const uint4*)rw)[p];
-        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-        const int len = dv.z & 0xffff, l4o = dv.z >> 16;
-        const int ver = dv.w & 0xff, proto = (dv.w >> 8) & 0xff;
-        if (l4o != 20 || ver != 4 || off > arena_len || (uint64_t)len > arena_len - off || len < 20) {
-            nat4_scalar(arena, arena_len, desc[p], rw[p], p, status, flags_out, STRICT ? 1 : 0);
-            continue;
-        }
-        const int mask = rv.w & 0xff;
-        const int fld = (proto == 6 || proto == 17) ? l4_field(proto) : -1;
-        const bool l4 = fld >= 0 && len - 20 >= fld + 2;
-        const int r0 = (int)(off & 15);
-        const uint32_t boff = (uint32_t)(off - (uint64_t)r0);
-        const int wend = r0 + (l4 ? 22 + fld : 24);   // window bytes needed
-        {
-            v4u v[4];
+    const uint32_t T = gridDim.x * blockDim.x;
+    for (uint32_t p0 = blockIdx.x * blockDim.x + threadIdx.x; p0 < n; p0 += W * T) {
+        uint4 dv[W], rv[W];
+        bool wide[W];
+        uint4 v[W][4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                v[k] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (k << 4) < wend ? boff + (k << 4) : kOutOfRange, 0, 0);
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            dv[i] = p < n ? ((const uint4*)desc)[p] : make_uint4(0, 0, 0, 0);
+            rv[i] = p < n ? ((const uint4*)rw)[p] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
+            const int len = dv[i].z & 0xffff, l4o = dv[i].z >> 16;
+            const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
+            wide[i] = p < n && !(l4o != 20 || ver != 4 || off > arena_len || (uint64_t)len > arena_len - off || len < 20);
+            const int fld = (proto == 6 || proto == 17) ? l4_field(proto) : -1;
+            const bool l4 = fld >= 0 && len - 20 >= fld + 2;
+            const int r0 = (int)(off & 15);
+            const uint32_t boff = (uint32_t)(off - (uint64_t)r0);
+            const int wend = wide[i] ? r0 + (l4 ? 22 + fld : 24) : 0;   // window bytes needed
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                s_win[threadIdx.x][2 * k] = make_uint2(v[k].x, v[k].y);
-                s_win[threadIdx.x][2 * k + 1] = make_uint2(v[k].z, v[k].w);
+                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (k << 4) < wend ? boff + (k << 4) : kOutOfRange, 0, 0);
+                v[i][k] = make_uint4(x.x, x.y, x.z, x.w);
             }
         }
-        const int b = r0;   // packet byte 0 inside the window
-        uint32_t ip_diff = 0, l4_diff = 0;
-        bool ip_dirty = false, l4_dirty = false;
-        if (mask & VPCSUM_NAT_SRC) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const uint32_t m = lds16(w, b + 12 + 2 * i);
-                const uint32_t mn = (((rv.x >> (16 * i)) & 0xff) << 8) | ((rv.x >> (16 * i + 8)) & 0xff);
-                ip_diff += (~m & 0xffff) + mn;
-                l4_diff += (~m & 0xffff) + mn;
-                sts16(w, b + 12 + 2 * i, mn);
-            }
-            ip_dirty = true; l4_dirty = true;
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            if (p < n)
+                nat4w_apply<STRICT>(arena, arena_len, desc, rw, p, dv[i], rv[i], wide[i], v[i], w,
+                                    &s_win[threadIdx.x], status, flags_out);
         }
-        if (mask & VPCSUM_NAT_DST) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const uint32_t m = lds16(w, b + 16 + 2 * i);
-                const uint32_t mn = (((rv.y >> (16 * i)) & 0xff) << 8) | ((rv.y >> (16 * i + 8)) & 0xff);
-                ip_diff += (~m & 0xffff) + mn;
-                l4_diff += (~m & 0xffff) + mn;
-                sts16(w, b + 16 + 2 * i, mn);
-            }
-            ip_dirty = true; l4_dirty = true;
-        }
-        if (mask & VPCSUM_NAT_DEC_TTL) {
-            const uint32_t m = lds16(w, b + 8);
-            const uint32_t mn = (((m >> 8) - 1) & 0xff) << 8 | (m & 0xff);
-            ip_diff += (~m & 0xffff) + mn;
-            sts16(w, b + 8, mn);
-            ip_dirty = true;
-        }
-        if (l4) {
-            if (mask & VPCSUM_NAT_SPORT) {
-                const uint32_t m = lds16(w, b + 20);
-                const uint32_t mn = ((rv.z & 0xff) << 8) | ((rv.z >> 8) & 0xff);
-                l4_diff += (~m & 0xffff) + mn;
-                sts16(w, b + 20, mn);
-                l4_dirty = true;
-            }
-            if (mask & VPCSUM_NAT_DPORT) {
-                const uint32_t m = lds16(w, b + 22);
-                const uint32_t mn = (((rv.z >> 16) & 0xff) << 8) | ((rv.z >> 24) & 0xff);
-                l4_diff += (~m & 0xffff) + mn;
-                sts16(w, b + 22, mn);
-                l4_dirty = true;
-            }
-        } else {
-            l4_dirty = false;
-        }
-        bool udp_zero = false;
-        if (!STRICT) {
-            if (ip_dirty) {
-                const uint32_t hc = lds16(w, b + 10);
-                sts16(w, b + 10, ~fold32((~hc & 0xffff) + fold32(ip_diff)) & 0xffff);
-            }
-            if (l4_dirty) {
-                const uint32_t hc = lds16(w, b + 20 + fld);
-                if (proto == 17 && hc == 0) {
-                    udp_zero = true;   // recomputed in full below, after the new header is stored
-                } else {
-                    uint32_t c = ~fold32((~hc & 0xffff) + fold32(l4_diff)) & 0xffff;
-                    if (proto == 17 && c == 0) c = 0xffff;
-                    sts16(w, b + 20 + fld, c);
-                }
-            }
-        }
-        // store back: dwords covering [8, 24) when anything in the IP header or ports changed,
-        // and the dword(s) of the L4 checksum field; a dword reaching past the packet end is
-        // stored bytewise (the neighbouring bytes may belong to another packet).
-        const uint32_t* wd = (const uint32_t*)w;
-        const int lim = r0 + len;
-        auto put = [&](int j) {
-            if (4 * j + 4 <= lim) {
-                *(__attribute__((address_space(1))) uint32_t*)(arena + boff + 4 * j) = wd[j];
-            } else {
-                for (int q = 4 * j; q < lim; ++q) arena[boff + q] = w[q];
-            }
-        };
-        if (ip_dirty || l4_dirty) {
-            const int j1 = (r0 + 23) >> 2;
-            for (int j = (r0 + 8) >> 2; j <= j1; ++j) put(j);
-            if (!STRICT && l4_dirty && !udp_zero) {
-                const int f = r0 + 20 + fld;
-                for (int j = max(f >> 2, j1 + 1); j <= (f + 1) >> 2; ++j) put(j);
-            }
-        }
-        const uint8_t fl = (ip_dirty ? VPCSUM_F_IP : 0) | (l4_dirty ? VPCSUM_F_L4 : 0);
-        if (STRICT) {
-            if (flags_out) flags_out[p] = fl;
-            continue;
-        }
-        if (udp_zero) {
-            // "no checksum" UDP: Java recomputes the full sum (UdpPacket.java:136-149)
-            uint8_t* l3 = arena + off;
-            uint8_t* l4p = l3 + 20;
-            const uint32_t seg = orient(lane_sum_range(l4p, l3 + len, l4p + fld), (int)((uintptr_t)l4p & 1));
-            const uint32_t ps = orient(lane_sum_range(l3 + 12, l3 + 20, nullptr), (int)((uintptr_t)l3 & 1));
-            uint32_t c = 0xffff - fold32(seg + ps + 17u + (uint32_t)(len - 20));
-            if (c == 0) c = 0xffff;
-            st16(l4p + fld, c);
-        }
-        if (status) status[p] = VPCSUM_S_DONE;
     }
 }
+
+constexpr int kNatWideLog2 = 1;   // packets per lane and iteration of k_nat4w: 2
 
 hipError_t launch_nat4(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const vpcsum_nat4_t* rw,
                        uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    uint32_t g = (n + 255) / 256;
+    const bool strict = (nat_mode & VPCSUM_NAT_STRICT_JAVA) != 0;
+    // nat_mode bits 12..14 (internal tuning): log2 packets per lane and iteration of the wide
+    // kernel + 1 (0 = default)
+    const int wsel = (int)((nat_mode >> 12) & 7u);
+    const int wl2 = wsel ? (wsel - 1 > 2 ? 2 : wsel - 1) : kNatWideLog2;
+    // one iteration of W packets per lane covers the batch when the chip holds the grid
+    uint32_t g = (n + (256u << wl2) - 1) / (256u << wl2);
     uint32_t cap = (uint32_t)num_cus(dev) * 8;
     if (g > cap) g = cap;
-    const bool strict = (nat_mode & VPCSUM_NAT_STRICT_JAVA) != 0;
     // nat_mode bit 8 (internal tuning): force the byte-access kernel
     const bool wide = !(nat_mode & 0x100u) && arena_len <= kMaxBufArena && !((uintptr_t)arena & 15);
     if (wide) {
-        if (strict)
-            hipLaunchKernelGGL(k_nat4w<true>, dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out);
-        else
-            hipLaunchKernelGGL(k_nat4w<false>, dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out);
+#define VPC_NAT(S, W) hipLaunchKernelGGL((k_nat4w<S, W>), dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out)
+        if (strict) {
+            if (wl2 == 0) VPC_NAT(true, 1); else if (wl2 == 1) VPC_NAT(true, 2); else VPC_NAT(true, 4);
+        } else {
+            if (wl2 == 0) VPC_NAT(false, 1); else if (wl2 == 1) VPC_NAT(false, 2); else VPC_NAT(false, 4);
+        }
+#undef VPC_NAT
     } else {
         hipLaunchKernelGGL(k_nat4, dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out,
                            strict ? 1 : 0);
