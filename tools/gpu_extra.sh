@@ -7,3 +7,4 @@ run() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "gpurun_out/$
 for w in ${WL:-c1 c3 c4}; do run bench_$w 300 python bench.py --workload $w --steps 100 --warmup 10 --cpu-budget 3; done
 run natbench 200 python tools/natbench.py
 [ "${HOSTPATH:-0}" = 1 ] && run hostpath 400 python tools/hostpath.py
+[ "${HOSTPATH:-0}" = 1 ] && { timeout -k 10 200 ./tools/flush_latency 2000 > gpurun_out/flush_latency.json 2> gpurun_out/flush_latency.err; echo "rc(flush_latency)=$?"; }
