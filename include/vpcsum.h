@@ -182,6 +182,15 @@ int vpcsum_ctx_wait(vpcsum_ctx_t* ctx, uint64_t ticket);
 int vpcsum_ctx_set_service(vpcsum_ctx_t* ctx, uint32_t idle_us);
 /* Counters of a context: batches the service ran, service grids launched (either may be NULL). */
 int vpcsum_ctx_stats(vpcsum_ctx_t* ctx, uint64_t* service_batches, uint64_t* service_launches);
+/* Ingress verify of a received batch (XDPIface.readable, XDPIface.java:281-314): the raw Ethernet
+ * frames at h_frame_off[i] (h_frame_len[i] bytes) of a registered arena are parsed on the GPU with
+ * the rules of EthernetPacket/Ipv4Packet/Ipv6Packet.from (as vpcsum_parse_ether_async) and
+ * verified (VPCSUM_MODE_VERIFY) where they lie, in one submission.  h_status[i]: S_DONE |
+ * S_IP_OK | S_L4_OK | S_UDP_NOCSUM, or S_BAD_DESC for a frame that does not parse; h_out (may
+ * be NULL): the sums the frames should carry.  Returns a ticket for vpcsum_ctx_wait. */
+int vpcsum_ctx_verify_frames(vpcsum_ctx_t* ctx, const uint8_t* h_arena, uint64_t arena_len,
+                             const uint64_t* h_frame_off, const uint32_t* h_frame_len, uint32_t n,
+                             uint32_t* h_out, uint8_t* h_status, uint64_t* ticket);
 /* Pipelined host->device->host throughput helper: processes a host arena of n fixed-stride
  * frames in `chunks` double-buffered pieces over two streams (H2D || kernel || D2H). */
 int vpcsum_ctx_pipeline(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint32_t stride, uint32_t copy_bytes,
@@ -221,6 +230,10 @@ int Java_io_vproxy_vpcsum_VPCsum_registerArena(PNIEnv_vpcsum_void* env, int64_t 
  *               MemorySegment out, MemorySegment status, int mode) -> long ticket */
 int Java_io_vproxy_vpcsum_VPCsum_submit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                         void* desc, int32_t n, void* out, void* status, int32_t mode);
+/* VPCsum.verifyFrames(long ctx, MemorySegment arena, long arenaLen, MemorySegment frameOff,
+ *                     MemorySegment frameLen, int n, MemorySegment out, MemorySegment status) -> long ticket */
+int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                              void* frameOff, void* frameLen, int32_t n, void* out, void* status);
 /* VPCsum.setService(long ctx, int idleUs) */
 int Java_io_vproxy_vpcsum_VPCsum_setService(PNIEnv_vpcsum_void* env, int64_t ctx, int32_t idleUs);
 /* VPCsum.waitFor(long ctx, long ticket) */

@@ -129,6 +129,18 @@ public final class GpuCsumBatch implements AutoCloseable {
         return status;
     }
 
+    /**
+     * Ingress verify straight from the RX ring (XDPIface.readable, XDPIface.java:281-314): the
+     * {@code count} received frames at umem offsets {@code frameOff} (u64 each) with lengths
+     * {@code frameLen} (u32 each) are parsed and verified on the GPU in one submission, without
+     * building descriptors in Java.  Returns one status byte per frame.
+     */
+    public MemorySegment verifyFrames(MemorySegment frameOff, MemorySegment frameLen, int count) throws IOException {
+        long t = VPCsum.get().verifyFrames(env, ctx, umem, umemLen, frameOff, frameLen, count, out, status);
+        VPCsum.get().waitFor(env, ctx, t);
+        return status;
+    }
+
     @Override
     public void close() {
         VPCsum.get().close(env, ctx);

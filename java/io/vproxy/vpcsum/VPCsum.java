@@ -126,6 +126,32 @@ public class VPCsum {
         }
     }
 
+    private static final MethodHandle verifyFramesMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(true),
+        "Java_io_vproxy_vpcsum_VPCsum_verifyFrames", long.class /* ctx */, MemorySegment.class /* arena */,
+        long.class /* arenaLen */, MemorySegment.class /* frameOff */, MemorySegment.class /* frameLen */, int.class /* n */,
+        MemorySegment.class /* out */, MemorySegment.class /* status */);
+
+    /** Ingress verify of a received batch: the raw Ethernet frames at frameOff[i] (u64, bytes into
+     * {@code arena}, which must be registered) of frameLen[i] (u32) bytes are parsed on the GPU with
+     * the rules of EthernetPacket/Ipv4Packet/Ipv6Packet.from and verified where they lie.
+     * status[i] gets S_IP_OK / S_L4_OK / S_UDP_NOCSUM (or S_BAD_DESC when the frame does not parse).
+     * Returns a ticket for {@link #waitFor}. */
+    public long verifyFrames(PNIEnv ENV, long ctx, MemorySegment arena, long arenaLen, MemorySegment frameOff,
+                             MemorySegment frameLen, int n, MemorySegment out, MemorySegment status) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) verifyFramesMH.invokeExact(ENV.MEMORY, ctx, arena, arenaLen, frameOff, frameLen, n, out, status);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+        return ENV.returnLong();
+    }
+
     private static final MethodHandle setServiceMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
         "Java_io_vproxy_vpcsum_VPCsum_setService", long.class /* ctx */, int.class /* idleUs */);
 

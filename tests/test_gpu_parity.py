@@ -695,3 +695,61 @@ def test_service_egress_batch(V, orc):
     assert np.array_equal(arena, want)
     assert batch.ctx.stats()["service_batches"] == batch.stats["flushes"] >= 5
     batch.close()
+
+
+def test_verify_frames_rx_batch(V, orc):
+    """Ingress verify of a received batch (ctx_verify_frames): raw Ethernet frames in a registered
+    arena are parsed and verified on the GPU; status and sums must equal the Java parse rules
+    (oracle parse_ether) followed by the oracle's verify, frame for frame."""
+    frames = []
+    for fn in sorted(os.listdir(os.path.join(GOLD, "pcap"))):
+        lt, pkts = read_pcap(os.path.join(GOLD, "pcap", fn))
+        if lt == 1:
+            frames += pkts
+    kats = json.load(open(os.path.join(GOLD, "kat.json")))["kats"]
+    frames += [bytes.fromhex(k["hex"]) for k in kats if k["layer"] == "ether"]
+    base = bytes.fromhex(kats[2]["hex"])
+    frames.append(base[:12] + b"\x81\x00\x00\x05" + base[12:])   # VLAN
+    frames.append(base[:30])                                     # truncated
+    frames.append(base[:12] + b"\x08\x06" + base[14:])           # ARP
+    # synthetic frames: C3 / C5 / FUZZ L3 packets behind an Ethernet header, valid and corrupted sums
+    rng = np.random.default_rng(12)
+    for wl in (O.SYNTH_C3, O.SYNTH_C5, O.SYNTH_FUZZ):
+        a, d = orc.synth(300, 9216, 14, wl, O.SEED, 50 + wl)
+        orc.process(a, d, O.MODE_COMPUTE, write=True)
+        for i in range(len(d)):
+            o, L = int(d[i]["l3_off"]), int(d[i]["l3_len"])
+            eth = bytearray(14)
+            eth[12:14] = b"\x08\x00" if d[i]["l3_ver"] == 4 else b"\x86\xdd"
+            f = bytearray(eth + bytes(a[o:o + L]))
+            if rng.random() < 0.2:
+                f[14 + L // 2] ^= 0xA5
+            frames.append(bytes(f))
+    offs, lens, arena = [], [], bytearray()
+    for f in frames:
+        arena += bytes(int(rng.integers(0, 64)))                 # any alignment
+        offs.append(len(arena))
+        lens.append(len(f))
+        arena += f
+    arena = np.frombuffer(bytes(arena) + bytes(4096), np.uint8).copy()
+    want_st = np.zeros(len(frames), np.uint8)
+    want_out = np.zeros(len(frames), np.uint32)
+    for i, f in enumerate(frames):
+        info, _ = O.parse_ether(f)
+        if info is None:
+            want_st[i] = O.S_BAD_DESC
+            continue
+        one = np.array([(offs[i] + info.l3_off, info.l3_len, info.l4_off, info.ver, info.proto,
+                         O.desc_flags_for(info), 0)], dtype=O.DESC_DTYPE)
+        o, st = orc.process(arena, one, O.MODE_VERIFY)
+        want_out[i], want_st[i] = o[0], st[0]
+    ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=4096)
+    ctx.register(arena)
+    before = arena.copy()
+    out, st = ctx.verify_frames(arena, np.array(offs), np.array(lens))
+    assert np.array_equal(st, want_st)
+    ok = (want_st & O.S_BAD_DESC) == 0
+    assert np.array_equal(out[ok], want_out[ok])
+    assert np.array_equal(arena, before)                         # verify never writes frames
+    assert int(np.sum(ok)) > 900 and int(np.sum((st & O.S_L4_OK) == 0)) > 100
+    ctx.close()

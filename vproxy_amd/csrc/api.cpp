@@ -71,6 +71,10 @@ struct Slot {
     vpcsum_desc_t* dh_desc = nullptr;  // device-side addresses of the pinned staging
     uint32_t* dh_out = nullptr;
     uint8_t* dh_status = nullptr;
+    uint64_t* h_foff = nullptr;        // pinned staging of received-frame offsets / lengths
+    uint32_t* h_flen = nullptr;
+    uint64_t* dh_foff = nullptr;
+    uint32_t* dh_flen = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     bool zero_copy = false;            // current batch ran on the host frames in place
@@ -272,6 +276,8 @@ static void slot_free(Slot& s) {
     if (s.h_out) (void)hipHostFree(s.h_out);
     if (s.h_status) (void)hipHostFree(s.h_status);
     if (s.h_arena) (void)hipHostFree(s.h_arena);
+    if (s.h_foff) (void)hipHostFree(s.h_foff);
+    if (s.h_flen) (void)hipHostFree(s.h_flen);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot();
@@ -357,6 +363,10 @@ int vpcsum_ctx_create(int device, uint64_t max_arena_bytes, uint32_t max_pkts, v
             (e = hipHostGetDevicePointer((void**)&s.dh_out, s.h_out, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&s.dh_status, s.h_status, 0)) != hipSuccess ||
             (e = hipHostMalloc((void**)&s.h_arena, max_arena_bytes + 64, 0)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_foff, (size_t)max_pkts * 8, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.h_flen, (size_t)max_pkts * 4, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&s.dh_foff, s.h_foff, 0)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&s.dh_flen, s.h_flen, 0)) != hipSuccess ||
             (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
             for (auto& t : c->slots) slot_free(t);
@@ -638,6 +648,46 @@ int vpcsum_ctx_wait(vpcsum_ctx_t* c, uint64_t ticket) {
     return slot_finish(c, s);
 }
 
+int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
+                             const uint32_t* h_frame_len, uint32_t n, uint32_t* h_out, uint8_t* h_status,
+                             uint64_t* ticket) {
+    if (!c || !ticket) return fail("vpcsum_ctx_verify_frames: NULL context or ticket");
+    if (n > c->max_pkts) return fail("vpcsum_ctx_verify_frames: %u frames > capacity %u", n, c->max_pkts);
+    if (n && (!h_arena || !h_frame_off || !h_frame_len || !h_status))
+        return fail("vpcsum_ctx_verify_frames: NULL arena, frame table or status");
+    std::lock_guard<std::mutex> lk(c->mu);
+    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
+    if (n && !base) return fail("vpcsum_ctx_verify_frames: the arena must be registered (vpcsum_ctx_register_arena)");
+    const uint64_t t = c->next_ticket++;
+    Slot& s = c->slots[t & 1];
+    if (s.busy && slot_finish(c, s) != 0) return -1;
+    if (n) {
+        // parse the frames where they lie (zero-copy), then verify the descriptors it built
+        memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
+        memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
+        VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.d_desc,
+                                     nullptr, s.stream),
+                  "parse launch");
+        VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, s.dh_out, s.dh_status, nullptr, VPCSUM_MODE_VERIFY, nullptr,
+                              n <= kZeroCopyWaveTeams ? 6 : 0, 0, s.stream),
+                  "verify launch");
+    }
+    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+    s.zero_copy = true;
+    s.svc_seq = 0;
+    s.busy = true;
+    s.ticket = t;
+    s.n = n;
+    s.mode = VPCSUM_MODE_VERIFY;
+    s.user_arena = nullptr;
+    s.user_desc = nullptr;
+    s.user_out = h_out;
+    s.user_status = h_status;
+    *ticket = t;
+    return 0;
+}
+
 int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint32_t copy_bytes,
                         const vpcsum_desc_t* h_desc, uint32_t n, uint32_t* h_out, uint32_t mode, uint32_t chunks) {
     if (!c || !h_arena || !h_desc || !h_out) return fail("vpcsum_ctx_pipeline: NULL argument");
@@ -726,6 +776,21 @@ int Java_io_vproxy_vpcsum_VPCsum_submit(PNIEnv_vpcsum_long* env, int64_t ctx, vo
 
 int Java_io_vproxy_vpcsum_VPCsum_waitFor(PNIEnv_vpcsum_void* env, int64_t ctx, int64_t ticket) {
     if (vpcsum_ctx_wait((vpcsum_ctx_t*)(intptr_t)ctx, (uint64_t)ticket) != 0) return pni_throw(env, "java.io.IOException");
+    return 0;
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                              void* frameOff, void* frameLen, int32_t n, void* out, void* status) {
+    if (n < 0 || arenaLen < 0) {
+        fail("verifyFrames: negative size");
+        return pni_throw(env, "java.lang.IllegalArgumentException");
+    }
+    uint64_t t = 0;
+    if (vpcsum_ctx_verify_frames((vpcsum_ctx_t*)(intptr_t)ctx, (const uint8_t*)arena, (uint64_t)arenaLen,
+                                 (const uint64_t*)frameOff, (const uint32_t*)frameLen, (uint32_t)n, (uint32_t*)out,
+                                 (uint8_t*)status, &t) != 0)
+        return pni_throw(env, "java.io.IOException");
+    env->return_ = (int64_t)t;
     return 0;
 }
 

@@ -35,10 +35,11 @@ EXPORTS = [
     "vpcsum_synth_async", "vpcsum_event_create", "vpcsum_event_destroy", "vpcsum_event_record",
     "vpcsum_event_elapsed_ms", "vpcsum_stream_sync", "vpcsum_ctx_create", "vpcsum_ctx_destroy",
     "vpcsum_ctx_register_arena", "vpcsum_ctx_unregister_arena", "vpcsum_ctx_submit", "vpcsum_ctx_wait",
-    "vpcsum_ctx_pipeline", "vpcsum_ctx_set_service", "vpcsum_ctx_stats",
+    "vpcsum_ctx_pipeline", "vpcsum_ctx_set_service", "vpcsum_ctx_stats", "vpcsum_ctx_verify_frames",
     "Java_io_vproxy_vpcsum_VPCsum_create", "Java_io_vproxy_vpcsum_VPCsum_registerArena",
     "Java_io_vproxy_vpcsum_VPCsum_submit", "Java_io_vproxy_vpcsum_VPCsum_waitFor",
     "Java_io_vproxy_vpcsum_VPCsum_close", "Java_io_vproxy_vpcsum_VPCsum_setService",
+    "Java_io_vproxy_vpcsum_VPCsum_verifyFrames",
 ]
 
 
@@ -77,6 +78,7 @@ def _declare(L):
         "vpcsum_ctx_unregister_arena": ([P, P], I),
         "vpcsum_ctx_set_service": ([P, U32], I),
         "vpcsum_ctx_stats": ([P, P, P], I),
+        "vpcsum_ctx_verify_frames": ([P, P, U64, P, P, U32, P, P, P], I),
         "vpcsum_ctx_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
         "vpcsum_ctx_wait": ([P, U64], I),
         "vpcsum_ctx_pipeline": ([P, P, U32, U32, P, U32, P, U32, U32], I),
@@ -218,6 +220,21 @@ class Context:
 
     def wait(self, ticket: int):
         _check(lib().vpcsum_ctx_wait(self.h, ticket), "vpcsum_ctx_wait")
+
+    def verify_frames(self, arena: np.ndarray, frame_off: np.ndarray, frame_len: np.ndarray):
+        """Ingress verify of received Ethernet frames in a registered arena: parsed and verified
+        on the GPU in one submission.  Returns (out, status) per frame."""
+        n = len(frame_off)
+        fo = np.ascontiguousarray(frame_off, dtype=np.uint64)
+        fl = np.ascontiguousarray(frame_len, dtype=np.uint32)
+        out = np.zeros(n, np.uint32)
+        status = np.zeros(n, np.uint8)
+        t = ctypes.c_uint64()
+        _check(lib().vpcsum_ctx_verify_frames(self.h, arena.ctypes.data, arena.nbytes, fo.ctypes.data, fl.ctypes.data,
+                                              n, out.ctypes.data, status.ctypes.data, ctypes.byref(t)),
+               "vpcsum_ctx_verify_frames")
+        self.wait(t.value)
+        return out, status
 
     def set_service(self, idle_us: int):
         """Low-latency flushes from registered arenas (persistent service grid); 0 = off."""
