@@ -47,6 +47,12 @@ extern "C" {
  * Ipv4Packet.java:219-234, Ipv6Packet.java:219-236), i.e. XDP's VP_CSUM_IP / VP_CSUM_UP. */
 #define VPCSUM_F_IP    0x01u /* IPv4 header checksum (field L3+10)                        */
 #define VPCSUM_F_L4    0x02u /* TCP(+16) / UDP(+6) / ICMP(+2) / ICMPv6(+2) checksum        */
+#define VPCSUM_F_L4P   0x08u /* checksum offload (VP_CSUM_UP_PSEUDO, SwitchUtils.java:297-316): the L4
+                              * field gets the folded, uncomplemented pseudo-header sum, the value
+                              * Linux stores for CHECKSUM_PARTIAL (the reference's pcap fixtures
+                              * hold 12 such TCP frames); the device adds the segment sum.  Not
+                              * with VPCSUM_F_L4; TCP / UDP / ICMPv6 only (ICMPv4 has no pseudo
+                              * header).  VERIFY compares the stored field with that value.    */
 #define VPCSUM_F_RAW   0x04u /* Utils.calculateChecksum(buf, len) over [l3_off, l3_off+l3_len);
                                 result in out bits 0..15; nothing else is interpreted       */
 

@@ -72,6 +72,15 @@ public final class GpuCsumBatch implements AutoCloseable {
      * dirty -> VP_CSUM_UP.
      */
     public boolean defer(PacketBuffer pkb, long frameOff) {
+        return defer(pkb, frameOff, false);
+    }
+
+    /**
+     * As {@link #defer(PacketBuffer, long)}; with {@code offload} (the TX queue completes L4
+     * checksums: VP_CSUM_UP_PSEUDO | VP_CSUM_XDP_OFFLOAD) the upper layer gets only its
+     * pseudo-header sum (F_L4P), ICMPv4 (no pseudo header) its full sum.
+     */
+    public boolean defer(PacketBuffer pkb, long frameOff, boolean offload) {
         if (!(pkb.pkt.getPacket() instanceof AbstractIpPacket ip)) {
             return false;
         }
@@ -84,7 +93,7 @@ public final class GpuCsumBatch implements AutoCloseable {
         var upper = ip.getPacket();
         boolean l4Kind = upper instanceof TcpPacket || upper instanceof UdpPacket || upper instanceof IcmpPacket;
         if (l4Kind && upper.isRequireUpdatingChecksum()) {
-            flags |= VPCsum.F_L4;
+            flags |= (offload && !(upper instanceof IcmpPacket icmp && !icmp.isIpv6())) ? VPCsum.F_L4P : VPCsum.F_L4;
         }
         if (flags == 0) {
             return false;

@@ -34,6 +34,8 @@ public class VPCsum {
     public static final int F_IP = 0x01;
     public static final int F_L4 = 0x02;
     public static final int F_RAW = 0x04;
+    /** checksum offload (VP_CSUM_UP_PSEUDO): L4 field = folded pseudo-header sum (CHECKSUM_PARTIAL) */
+    public static final int F_L4P = 0x08;
     // status bits
     public static final int S_IP_OK = 0x01;
     public static final int S_L4_OK = 0x02;

@@ -175,7 +175,15 @@ void orc_process_one(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc
     } else {
         bad = 1;
     }
-    int do_l4 = 0;
+    int do_l4 = 0, psonly = 0;
+    if (!bad && (d->flags & VPCSUM_F_L4P)) {
+        /* checksum offload: pseudo-header sum only (CHECKSUM_PARTIAL convention) */
+        int fld = orc_l4_field(d->l4_proto);
+        if ((d->flags & VPCSUM_F_L4) || fld < 0 || d->l4_proto == 1) bad = 1;
+        else if (d->l3_ver == 4 && d->l4_proto == 58) bad = 1;
+        else if (len - d->l4_off < (uint32_t)fld + 2) bad = 1;
+        else do_l4 = 1, psonly = 1;
+    }
     if (!bad && (d->flags & VPCSUM_F_L4)) {
         int fld = orc_l4_field(d->l4_proto);
         if (fld < 0) bad = 1;
@@ -199,12 +207,24 @@ void orc_process_one(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc
     }
     if (do_l4) {
         int fld = orc_l4_field(d->l4_proto);
-        orc_l4_csum(l3, len, d->l4_off, d->l3_ver, d->l4_proto, &l4c);
+        if (psonly) {
+            uint32_t seg_len = len - d->l4_off;
+            uint8_t ph[40];
+            if (d->l3_ver == 4) {
+                orc_pseudo4(l3, d->l4_proto, seg_len, ph);
+                l4c = orc_csum_intermediate(0, ph, 12);
+            } else {
+                orc_pseudo6(l3, d->l4_proto, seg_len, ph);
+                l4c = orc_csum_intermediate(0, ph, 40);
+            }
+        } else {
+            orc_l4_csum(l3, len, d->l4_off, d->l3_ver, d->l4_proto, &l4c);
+        }
         if (mode & VPCSUM_MODE_VERIFY) {
             const uint8_t* f = l3 + d->l4_off + fld;
             uint32_t stored = ((uint32_t)f[0] << 8) | f[1];
             if (stored == l4c) st |= VPCSUM_S_L4_OK;
-            if (d->l4_proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+            if (!psonly && d->l4_proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
         }
     }
     if ((mode & VPCSUM_MODE_WRITE) && arena_w) {

@@ -28,7 +28,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "liborc.so")
 
-F_IP, F_L4, F_RAW = 0x01, 0x02, 0x04
+F_IP, F_L4, F_RAW, F_L4P = 0x01, 0x02, 0x04, 0x08
 S_IP_OK, S_L4_OK, S_UDP_NOCSUM, S_DONE, S_BAD_DESC = 0x01, 0x02, 0x04, 0x40, 0x80
 MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
 NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL = 0x01, 0x02, 0x04, 0x08, 0x10
@@ -200,10 +200,21 @@ def desc_flags_for(info: L3Info, want_ip=True, want_l4=True) -> int:
     return f
 
 
+def pseudo_partial(l3: bytes, info: L3Info) -> int:
+    """VPCSUM_F_L4P (checksum offload, XDPConsts.VP_CSUM_UP_PSEUDO): the folded, uncomplemented
+    pseudo-header sum the L4 field holds for CHECKSUM_PARTIAL; Utils.calculateChecksumIntermediate
+    over Utils.buildPseudoIPv4/IPv6Header (Utils.java:758-797)."""
+    seg = info.l3_len - info.l4_off
+    ph = pseudo_ipv4(l3, info.proto, seg) if info.ver == 4 else pseudo_ipv6(l3, info.proto, seg)
+    return csum_intermediate(0, ph, len(ph))
+
+
 def pure_process(l3: bytes, info: L3Info, flags: int) -> tuple[int, int]:
     """Pure-Python (ip_csum, l4_csum) for one parsed L3 packet."""
     ipc = ipv4_header_csum(l3, info.l4_off) if flags & F_IP else 0
     l4c = l4_csum(l3, info.l3_len, info.l4_off, info.ver, info.proto) if flags & F_L4 else 0
+    if flags & F_L4P:
+        l4c = pseudo_partial(l3, info)
     return ipc, l4c
 
 

@@ -753,3 +753,58 @@ def test_verify_frames_rx_batch(V, orc):
     assert np.array_equal(arena, before)                         # verify never writes frames
     assert int(np.sum(ok)) > 900 and int(np.sum((st & O.S_L4_OK) == 0)) > 100
     ctx.close()
+
+
+# ---- checksum offload: pseudo-header partial sums (VPCSUM_F_L4P, VP_CSUM_UP_PSEUDO) ----
+
+@pytest.mark.parametrize("team", [0, 2, 6, 40, 45, 46, 47, 62])
+@pytest.mark.parametrize("workload", [O.SYNTH_C3, O.SYNTH_C4, O.SYNTH_FUZZ])
+def test_l4_pseudo_partial(V, orc, team, workload):
+    """F_L4P on every packet (with and without F_IP), all modes, against the oracle: the field
+    gets the folded pseudo-header sum (CHECKSUM_PARTIAL); ICMPv4 and F_L4P|F_L4 are rejected."""
+    stride = 9216
+    n = 700
+    arena, desc = orc.synth(n, stride, 5, workload, O.SEED, 90 + workload)
+    rng = np.random.default_rng(workload)
+    desc = desc.copy()
+    f = np.where(desc["l3_ver"] == 4, O.F_IP, 0) | O.F_L4P
+    f[rng.random(n) < 0.1] |= O.F_L4        # invalid combination -> BAD
+    f[rng.random(n) < 0.2] &= ~O.F_IP
+    desc["flags"] = f
+    for mode, write in ((O.MODE_COMPUTE, False), (O.MODE_VERIFY, False), (O.MODE_COMPUTE, True)):
+        out, st, after = gpu_compute(V, arena, desc, mode, team, write=write)
+        a2 = arena.copy()
+        oout, ost = orc.process(a2, desc, mode, write=write)
+        assert np.array_equal(st, ost), (mode, write)
+        assert np.array_equal(out, oout), (mode, write)
+        if write:
+            assert np.array_equal(after, a2)
+    # after WRITE every F_L4P packet verifies as partial
+    orc.process(arena, desc, O.MODE_COMPUTE, write=True)
+    _, st, _ = gpu_compute(V, arena, desc, O.MODE_VERIFY, team)
+    good = (st & O.S_BAD_DESC) == 0
+    assert np.all(st[good] & O.S_L4_OK)
+
+
+def test_l4_pseudo_partial_pcap(V, orc):
+    """The reference's CHECKSUM_PARTIAL pcap frames verify under F_L4P on the GPU."""
+    partial = 0
+    for fn in sorted(os.listdir(os.path.join(GOLD, "pcap"))):
+        lt, pkts = read_pcap(os.path.join(GOLD, "pcap", fn))
+        for p in pkts:
+            off = l3_offset(lt, p)
+            if off is None:
+                continue
+            info, err = O.parse_l3(p, off, len(p) - off)
+            if info is None or info.proto != O.IP_PROTOCOL_TCP:
+                continue
+            arena = np.frombuffer(p + bytes(64), np.uint8).copy()
+            desc = np.array([(off, info.l3_len, info.l4_off, info.ver, info.proto, O.F_L4, 0),
+                             (off, info.l3_len, info.l4_off, info.ver, info.proto, O.F_L4P, 0)], dtype=O.DESC_DTYPE)
+            out, st, _ = gpu_compute(V, arena, desc, O.MODE_VERIFY)
+            oout, ost = orc.process(arena, desc, O.MODE_VERIFY)
+            assert np.array_equal(out, oout) and np.array_equal(st, ost)
+            if not st[0] & O.S_L4_OK:
+                assert st[1] & O.S_L4_OK
+                partial += 1
+    assert partial == 12

@@ -91,7 +91,7 @@ PCAP_EXPECT = {
 @pytest.mark.parametrize("fn", sorted(PCAP_EXPECT))
 def test_pcap_fixtures(orc, fn):
     lt, pkts = read_pcap(os.path.join(GOLD, "pcap", fn))
-    nip = ipok = nl4 = l4ok = 0
+    nip = ipok = nl4 = l4ok = npartial = 0
     for p in pkts:
         off = l3_offset(lt, p)
         if off is None:
@@ -115,6 +115,13 @@ def test_pcap_fixtures(orc, fn):
                 assert info.proto == O.IP_PROTOCOL_TCP
                 ph = O.pseudo_ipv4(l3, info.proto, info.l3_len - info.l4_off)
                 assert stored == O.csum_intermediate(0, ph, len(ph))
+                # ... which is what VPCSUM_F_L4P (VP_CSUM_UP_PSEUDO) computes: pins its parity
+                assert O.pure_process(l3, info, O.F_L4P)[1] == stored
+                npartial += 1
+                dp = np.zeros(1, O.DESC_DTYPE)
+                dp[0] = (off, info.l3_len, info.l4_off, info.ver, info.proto, O.F_L4P, 0)
+                outp, stp = orc.process(np.frombuffer(p, np.uint8).copy(), dp, O.MODE_VERIFY)
+                assert outp[0] >> 16 == stored and stp[0] & O.S_L4_OK
             # C oracle agrees with the pure-Python one on every frame
             arena = np.frombuffer(p, np.uint8).copy()
             d = np.zeros(1, O.DESC_DTYPE)
@@ -123,6 +130,7 @@ def test_pcap_fixtures(orc, fn):
             assert out[0] >> 16 == c4 and out[0] & 0xFFFF == c
             assert bool(st[0] & O.S_L4_OK) == (c4 == stored)
     assert (nip, ipok, nl4, l4ok) == PCAP_EXPECT[fn]
+    assert npartial == nl4 - l4ok      # every TCP frame that fails verify is CHECKSUM_PARTIAL
 
 
 def test_pure_vs_c_random(orc):

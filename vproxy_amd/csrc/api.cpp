@@ -487,7 +487,7 @@ static int slot_finish(vpcsum_ctx* c, Slot& s) {
             uint8_t* l3 = s.user_arena + d.l3_off;
             const uint32_t w = s.h_out[i];
             if (d.flags & VPCSUM_F_IP) { l3[10] = (uint8_t)(w >> 8); l3[11] = (uint8_t)w; }
-            if (d.flags & VPCSUM_F_L4) {
+            if (d.flags & (VPCSUM_F_L4 | VPCSUM_F_L4P)) {
                 const int fld = d.l4_proto == 6 ? 16 : d.l4_proto == 17 ? 6 : 2;
                 l3[d.l4_off + fld] = (uint8_t)(w >> 24);
                 l3[d.l4_off + fld + 1] = (uint8_t)(w >> 16);

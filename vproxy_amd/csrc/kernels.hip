@@ -169,15 +169,17 @@ __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64
         // ---- validate (never read or write outside the arena) ----
         bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
         const bool raw = (fl & VPCSUM_F_RAW) != 0;
-        bool do_ip = false, do_l4 = false;
+        bool do_ip = false, do_l4 = false, psonly = false;
         int fld = -1;
         if (!bad && !raw) {
             if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
             else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
             else bad = true;
-            if (!bad && (fl & VPCSUM_F_L4)) {
+            if (!bad && (fl & (VPCSUM_F_L4 | VPCSUM_F_L4P))) {
+                psonly = (fl & VPCSUM_F_L4P) != 0;
                 fld = l4_field(proto);
                 if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
+                else if (psonly && ((fl & VPCSUM_F_L4) || proto == 1)) bad = true;
                 else do_l4 = true;
             }
             if (!bad && (fl & VPCSUM_F_IP)) {
@@ -197,11 +199,15 @@ __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64
         const uint4* base = (const uint4*)((uintptr_t)l3 & ~(uintptr_t)15);
         PktPlan pl;
         pl.r0 = (int)((uintptr_t)l3 & 15);
-        const int need = (raw || do_l4) ? len : (do_ip ? l4o : 0);
+        // pseudo-only (F_L4P): the IP header holds the pseudo addresses, the segment is not read
+        const int need = psonly ? l4o + fld + 2 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
         pl.nch = (pl.r0 + need + 15) >> 4;
         if (raw) {
             pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
             pl.fast_lo = (pl.r0 + 15) & ~15;
+        } else if (psonly) {
+            pl.l4lo = 0; pl.l4hi = 0; pl.fa = pl.r0 + l4o + fld;
+            pl.fast_lo = 1 << 30;
         } else if (do_l4) {
             pl.l4lo = pl.r0 + l4o; pl.l4hi = pl.r0 + len; pl.fa = pl.r0 + l4o + fld;
             pl.fast_lo = (pl.fa + 2 + 15) & ~15;
@@ -287,15 +293,19 @@ __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64
                         const int pproto = proto;   // Consts.IP_PROTOCOL_* of the L4 class
                         tot += orient(fold32(s_ps), pl.r0) + (uint32_t)pproto + (l4len & 0xffff) + (l4len >> 16);
                     }
-                    l4c = 0xffff - fold32(tot);
-                    if (proto == 17 && l4c == 0) l4c = 0xffff;
+                    if (psonly) {
+                        l4c = fold32(tot);   // CHECKSUM_PARTIAL: uncomplemented
+                    } else {
+                        l4c = 0xffff - fold32(tot);
+                        if (proto == 17 && l4c == 0) l4c = 0xffff;
+                    }
                 }
                 if (VERIFY) {
                     if (do_ip && orient(fold32(s_stip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
                     if (do_l4) {
                         const uint32_t stored = orient(fold32(s_stl4), pl.fa);
                         if (stored == l4c) st |= VPCSUM_S_L4_OK;
-                        if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                        if (!psonly && proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
                     }
                 }
                 if (arena_w) {
@@ -590,15 +600,17 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
 
         bool bad = !live || off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
         const bool raw = (fl & VPCSUM_F_RAW) != 0;
-        bool do_ip = false, do_l4 = false;
+        bool do_ip = false, do_l4 = false, psonly = false;
         int fld = -1;
         if (!bad && !raw) {
             if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
             else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
             else bad = true;
-            if (!bad && (fl & VPCSUM_F_L4)) {
+            if (!bad && (fl & (VPCSUM_F_L4 | VPCSUM_F_L4P))) {
+                psonly = (fl & VPCSUM_F_L4P) != 0;
                 fld = l4_field(proto);
                 if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
+                else if (psonly && ((fl & VPCSUM_F_L4) || proto == 1)) bad = true;
                 else do_l4 = true;
             }
             if (!bad && (fl & VPCSUM_F_IP)) {
@@ -613,11 +625,15 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
             PktPlan pl;
             pl.r0 = r0;
             const uint32_t boff = (uint32_t)(off & ~(uint64_t)15);
-            const int need = bad ? 0 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
+            // pseudo-only (F_L4P): the IP header holds the pseudo addresses, the segment is not read
+            const int need = bad ? 0 : psonly ? l4o + fld + 2 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
             pl.nch = bad ? 0 : (r0 + need + 15) >> 4;
             if (raw) {
                 pl.l4lo = r0; pl.l4hi = r0 + len; pl.fa = -64;
                 pl.fast_lo = (r0 + 15) & ~15;
+            } else if (psonly) {
+                pl.l4lo = 0; pl.l4hi = 0; pl.fa = r0 + l4o + fld;
+                pl.fast_lo = 1 << 30;
             } else if (do_l4) {
                 pl.l4lo = r0 + l4o; pl.l4hi = r0 + len; pl.fa = r0 + l4o + fld;
                 pl.fast_lo = (pl.fa + 2 + 15) & ~15;
@@ -643,7 +659,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                 }
                 if (do_l4) {
                     F_l4 = hw_bit(pl.fa >> 1);
-                    B_l4 = hw_range((r0 + l4o) >> 1, (r0 + need + 1) >> 1) & ~F_l4;
+                    B_l4 = psonly ? 0u : hw_range((r0 + l4o) >> 1, (r0 + need + 1) >> 1) & ~F_l4;
                     if (proto != 1) B_l4 |= (ver == 4) ? hw_range(r0h + 6, r0h + 10) : hw_range(r0h + 4, r0h + 20);
                 }
             }
@@ -700,15 +716,19 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                             const uint32_t l4len = (uint32_t)(len - l4o);
                             tot += orient(sums.z, r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
                         }
-                        l4c = 0xffff - fold32(tot);
-                        if (proto == 17 && l4c == 0) l4c = 0xffff;
+                        if (psonly) {
+                            l4c = fold32(tot);   // CHECKSUM_PARTIAL: uncomplemented
+                        } else {
+                            l4c = 0xffff - fold32(tot);
+                            if (proto == 17 && l4c == 0) l4c = 0xffff;
+                        }
                     }
                     if (VERIFY) {
                         if (do_ip && orient(sums.w >> 16, r0) == ipc) st |= VPCSUM_S_IP_OK;
                         if (do_l4) {
                             const uint32_t stored = orient(sums.w & 0xffff, r0 + l4o + fld);
                             if (stored == l4c) st |= VPCSUM_S_L4_OK;
-                            if (proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                            if (!psonly && proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
                         }
                     }
                     if (arena_w) {

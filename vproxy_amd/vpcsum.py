@@ -16,7 +16,7 @@ import numpy as np
 
 from .build import LIB
 
-F_IP, F_L4, F_RAW = 0x01, 0x02, 0x04
+F_IP, F_L4, F_RAW, F_L4P = 0x01, 0x02, 0x04, 0x08
 S_IP_OK, S_L4_OK, S_UDP_NOCSUM, S_DONE, S_BAD_DESC = 0x01, 0x02, 0x04, 0x40, 0x80
 MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
 NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL = 0x01, 0x02, 0x04, 0x08, 0x10

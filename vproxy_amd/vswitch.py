@@ -20,14 +20,17 @@ ETHER_TYPE_IPv4, ETHER_TYPE_IPv6, ETHER_TYPE_8021Q = 0x0800, 0x86DD, 0x8100
 L4_WITH_CSUM = {6, 17, 1, 58}
 
 
-def checksum_flags_for(is_ipv4: bool, ip_dirty: bool, upper_proto: int, upper_dirty: bool) -> int:
+def checksum_flags_for(is_ipv4: bool, ip_dirty: bool, upper_proto: int, upper_dirty: bool,
+                       offload: bool = False) -> int:
     """SwitchUtils.checksumFlagsFor: which sums a frame needs recomputed.  IPv6 has no header
-    checksum (Ipv6Packet.__updateChecksum only recurses, Ipv6Packet.java:214-217)."""
+    checksum (Ipv6Packet.__updateChecksum only recurses, Ipv6Packet.java:214-217).  With
+    ``offload`` (checksum offload on the TX queue: VP_CSUM_UP_PSEUDO | VP_CSUM_XDP_OFFLOAD) the
+    upper layer gets only its pseudo-header sum (F_L4P); ICMPv4 has none and is summed in full."""
     f = 0
     if is_ipv4 and ip_dirty:
         f |= V.F_IP
     if upper_dirty and upper_proto in L4_WITH_CSUM and not (is_ipv4 and upper_proto == 58):
-        f |= V.F_L4
+        f |= V.F_L4P if offload and upper_proto != 1 else V.F_L4
     return f
 
 
