@@ -118,8 +118,13 @@ int main(int argc, char** argv) {
 #define PK(T, U, NT, BPC)                                                                      \
     snprintf(nm, sizeof nm, "pkt1504/2048 team=%d unr=%d nt=%d bpc=%d", T, U, NT, BPC);         \
     timeit(nm, (double)nfr * pb, [&] { hipLaunchKernelGGL((k_pkt<T, U, NT>), dim3(cus * BPC), dim3(256), 0, 0, buf, nfr, stride, pb, sink); });
-    if (argc > 1) {   // short mode: the packet pattern with nt loads only
-        PK(16, 8, true, 8) PK(8, 12, true, 8) PK(8, 6, true, 8) PK(8, 12, true, 4) PK(8, 6, true, 16) PK(4, 12, true, 8) PK(16, 8, true, 4)
+    if (argc > 1) {   // short mode: the packet pattern with nt loads only, strided vs packed
+        PK(16, 8, true, 8) PK(16, 8, true, 2) PK(8, 6, true, 2) PK(8, 6, true, 8)
+#define PKS(T, U, BPC, STR)                                                                          \
+    snprintf(nm, sizeof nm, "pkt1504/%d team=%d unr=%d nt=1 bpc=%d", STR, T, U, BPC);                \
+    timeit(nm, (double)nfr * pb, [&] { hipLaunchKernelGGL((k_pkt<T, U, true>), dim3(cus * BPC), dim3(256), 0, 0, buf, nfr, STR, pb, sink); });
+        PKS(16, 8, 8, 1504) PKS(16, 8, 2, 1504) PKS(8, 6, 2, 1504) PKS(16, 8, 8, 1536) PKS(16, 8, 2, 1536)
+        SL(8, true, 2) SL(8, true, 8)
         return 0;
     }
     PK(16, 8, false, 8) PK(16, 8, true, 8) PK(32, 4, false, 8) PK(64, 2, false, 8) PK(64, 2, false, 16) PK(16, 8, false, 4) PK(8, 12, false, 8)

@@ -791,8 +791,11 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                 const uint64_t w = __hip_atomic_load(&mb->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (w & kSvcStop) break;
                 if ((uint32_t)w != seen) { cmd = w; break; }
-                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
-                __builtin_amdgcn_s_sleep(1);
+                const uint64_t idle = __builtin_amdgcn_s_memrealtime() - t0;
+                if (idle > idle_ticks) break;
+                // back off after 50 us without a batch: ~1 us more latency, far fewer PCIe reads
+                if (idle > 5000) __builtin_amdgcn_s_sleep(40);
+                else __builtin_amdgcn_s_sleep(1);
             }
             // acquire at system scope: the frames, descriptors and parameters the host wrote
             // before the command word are read fresh (no kernel boundary invalidates caches here)
