@@ -808,3 +808,39 @@ def test_l4_pseudo_partial_pcap(V, orc):
                 assert st[1] & O.S_L4_OK
                 partial += 1
     assert partial == 12
+
+
+def test_arena_beyond_4gib(V, orc):
+    """Arenas past the 32-bit buffer-descriptor range (> 4 GiB, as a umem of a large switch can
+    be): packets below and above 4 GiB go through the global-load fallback, bit-exact."""
+    import torch
+    n, stride = 1500, 9216                                     # FUZZ frames reach 9000 B
+    a, d = orc.synth(n, stride, 6, O.SYNTH_FUZZ, O.SEED, 4444)
+    want, want_st = orc.process(a, d, O.MODE_VERIFY)
+    big = torch.zeros((5 << 30) + 4096, dtype=torch.uint8, device="cuda")
+    rng = np.random.default_rng(4)
+    bases = np.sort(rng.choice(((5 << 30) - (1 << 20)) // 16384, n, replace=False)) * 16384 + 8
+    bases[: n // 3] = np.arange(n // 3) * 16384 + 8          # a third below 4 GiB
+    dg = d.copy()
+    src = torch.from_numpy(a).cuda()
+    for i in range(n):
+        big[int(bases[i]): int(bases[i]) + stride] = src[i * stride:(i + 1) * stride]
+        dg[i]["l3_off"] = int(bases[i]) + int(d[i]["l3_off"]) - i * stride
+    assert int(dg["l3_off"].max()) > (4 << 30)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    dt = V.desc_to_tensor(dg)
+    V.compute(big, dt, n, out, st, O.MODE_VERIFY)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    # in-place writes land at the right > 4 GiB addresses
+    a2 = a.copy()
+    orc.process(a2, d, O.MODE_COMPUTE, write=True)
+    V.compute(big, dt, n, out, None, O.MODE_WRITE)
+    torch.cuda.synchronize()
+    for i in rng.choice(n, 64, replace=False):
+        got = big[int(bases[i]): int(bases[i]) + stride].cpu().numpy()
+        assert np.array_equal(got, a2[i * stride:(i + 1) * stride]), i
+    del big
+    torch.cuda.empty_cache()
