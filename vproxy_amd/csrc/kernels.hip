@@ -417,9 +417,11 @@ __device__ __forceinline__ uint32_t buf_records(uint64_t arena_len) {
 // (C3) no longer pays the longest of PPI random packets per iteration.
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // LDS instructions of one wave execute in program order, so lanes exchanging data through
+    // LDS only need the compiler not to move accesses across this point (no memory fence: a
+    // fence makes the compiler wait for every outstanding store, vmcnt(0), once per unit)
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    asm volatile("" ::: "memory");
 }
 
 // Fast-class trips of one team over its packet's chunks [0, nch): U loads per lane issued
@@ -578,6 +580,9 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         }
     }
     const uint32_t wstride = grid * 4u * 64u;
+    // first descriptor in registers before the loop, so that the loop head holds no wait that
+    // the back edge (this unit's stores pending) would have to honour too
+    asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
     for (uint32_t Pn; P0 < n; P0 = Pn) {
         // ---- phase A: this lane's packet ----
         const uint4 dv = dnext;
@@ -698,6 +703,10 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
             stream_tier<TEAM, U, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, 64);
         }
         wave_sync_lds();
+        // The next unit's descriptor (loaded a whole unit ago) is taken into registers here,
+        // before this unit's stores: vmcnt counts loads and stores together, so a wait for it
+        // after the stores would stall the wave until they complete, once per unit.
+        asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
 
         // ---- phase C: finalize this lane's packet ----
         uint32_t res_out = 0, res_st = VPCSUM_S_BAD_DESC;
