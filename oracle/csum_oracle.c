@@ -318,6 +318,37 @@ void orc_nat4_java(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, c
     if (status) *status = VPCSUM_S_DONE;
 }
 
+/* Batch of the above, split over threads (the CPU baseline of BASELINE config C5; frames of
+ * one batch must not overlap). */
+typedef struct {
+    uint8_t* arena; uint64_t arena_len; const vpcsum_desc_t* d; const vpcsum_nat4_t* rw;
+    uint8_t* status; uint32_t lo, hi;
+} orc_nat_job;
+
+static void* orc_nat_job_run(void* p) {
+    orc_nat_job* j = (orc_nat_job*)p;
+    for (uint32_t i = j->lo; i < j->hi; ++i)
+        orc_nat4_java(j->arena, j->arena_len, j->d + i, j->rw + i, j->status ? j->status + i : NULL);
+    return NULL;
+}
+
+int orc_nat4_java_batch(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const vpcsum_nat4_t* rw,
+                        uint32_t n, uint8_t* status, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    orc_nat_job jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t].arena = arena; jobs[t].arena_len = arena_len; jobs[t].d = d; jobs[t].rw = rw;
+        jobs[t].status = status;
+        jobs[t].lo = (uint32_t)((uint64_t)n * t / nthreads);
+        jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
+        if (pthread_create(&th[t], NULL, orc_nat_job_run, &jobs[t]) != 0) return -1;
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    return 0;
+}
+
 /* ---------------------------------------------------------------------------------------- */
 /* Synthetic workloads (splitmix64, seed 0x20241020).  Counter-based so any    */
 /* packet can be regenerated independently; libvpcsum's GPU generator must match this.      */

@@ -243,6 +243,8 @@ class Oracle:
         L.orc_csum_intermediate.restype = U32
         L.orc_synth_batch.argtypes = [P, U32, U32, U32, U32, U64, U64, P]
         L.orc_nat4_java.argtypes = [P, U64, P, P, P]
+        L.orc_nat4_java_batch.argtypes = [P, U64, P, P, U32, P, ctypes.c_int]
+        L.orc_nat4_java_batch.restype = ctypes.c_int
         L.orc_rng.argtypes = [U64, U64, U64]
         L.orc_rng.restype = U64
         self.L = L
@@ -277,11 +279,14 @@ class Oracle:
         self.L.orc_synth_batch(self._p(arena), n, stride, l3_pad, workload, seed, first_index, self._p(desc))
         return arena, desc
 
-    def nat4_java(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray):
+    def nat4_java(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray, threads: int = 1):
+        """In order on one thread; threads > 1 needs frames that do not overlap."""
         status = np.zeros(len(desc), np.uint8)
-        for i in range(len(desc)):
-            self.L.orc_nat4_java(self._p(arena), arena.nbytes, self._p(desc[i:i + 1]), self._p(rw[i:i + 1]),
-                                 self._p(status[i:i + 1]))
+        desc = np.ascontiguousarray(desc)
+        rw = np.ascontiguousarray(rw)
+        rc = self.L.orc_nat4_java_batch(self._p(arena), arena.nbytes, self._p(desc), self._p(rw), len(desc),
+                                        self._p(status), threads)
+        assert rc == 0
         return status
 
     def rng(self, seed: int, pkt: int, word: int) -> int:

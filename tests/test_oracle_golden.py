@@ -210,3 +210,21 @@ def test_nat_golden_matches_pure_python():
             l3[f:f + 2] = c4.to_bytes(2, "big")
         fr[off:] = l3
         assert bytes(fr).hex() == c["after"], (c["kat"], c["rewrite"])
+
+
+def test_nat_batch_threads_match_sequential(orc):
+    """The threaded batch NAT (natbench's CPU baseline) equals the in-order single-thread run."""
+    m = 512
+    arena, desc = orc.synth(m, 2048, 0, O.SYNTH_C5, O.SEED, 0)
+    orc.process(arena, desc, write=True)
+    rw = np.random.default_rng(7).integers(0, 256, (m, 16), dtype=np.uint8)
+    rw[:, 12] = np.random.default_rng(8).integers(0, 32, m, dtype=np.uint8)
+    rw[:, 13:] = 0
+    a1, a4 = arena.copy(), arena.copy()
+    s1 = orc.nat4_java(a1, desc, rw, threads=1)
+    s4 = orc.nat4_java(a4, desc, rw, threads=4)
+    assert np.array_equal(a1, a4) and np.array_equal(s1, s4)
+    assert not np.array_equal(a1, arena)
+    # every rewritten packet still verifies (IP and L4 sums recomputed in full)
+    _, st = orc.process(a1, desc, mode=O.MODE_VERIFY)
+    assert np.all(st & O.S_IP_OK) and np.all(st & O.S_L4_OK)

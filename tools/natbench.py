@@ -32,4 +32,28 @@ for name, mode in modes:
     e1.record()
     ms = e0.elapsed_ms(e1) / it
     res[name] = {"ms": round(ms, 4), "Mpps": round(n / ms / 1e3, 1), "GBps_at_72B": round(n * 72 / ms / 1e6, 1)}
+
+if "--no-cpu" not in sys.argv:
+    # CPU baseline (BASELINE C5): the oracle's Java-semantics rewrite (setters + full recompute,
+    # SwitchUtils.java:522-542) on a bounded sample of the same workload, 1 and 16 threads
+    from oracle import oracle as O  # noqa: E402
+    orc = O.Oracle()
+    m = 1 << 18
+    a_np, d_np = orc.synth(m, stride, 0, O.SYNTH_C5, O.SEED, 0)
+    orc.process(a_np, d_np, write=True)
+    rw_np = rw[:m].cpu().numpy()
+    cpu = {"packets": m, "kind": "port"}
+    for th in (1, 16):
+        a = a_np.copy()
+        t = time.perf_counter()
+        orc.nat4_java(a, d_np, rw_np, threads=th)
+        dt = time.perf_counter() - t
+        cpu[f"strict_java_{th}t_Mpps"] = round(m / dt / 1e6, 2)
+    # the GPU's strict-Java result on the same packets must equal the oracle's
+    g = torch.from_numpy(a_np.copy()).cuda()
+    gd = torch.from_numpy(d_np.view(np.uint8).copy()).cuda()
+    gst = torch.zeros(m, dtype=torch.uint8, device="cuda")
+    V.nat4(g, gd, rw[:m].contiguous(), m, gst, V.NAT_STRICT_JAVA)
+    cpu["gpu_equal"] = bool(np.array_equal(g.cpu().numpy(), a))
+    res["cpu_baseline"] = cpu
 print(json.dumps(res))
