@@ -142,6 +142,14 @@ int vpcsum_parse_ether_async(const uint8_t* d_arena, uint64_t arena_len,
 int vpcsum_read_probe_async(const uint8_t* d_buf, uint64_t bytes, uint32_t* d_sink,
                             uint32_t grid, void* stream);
 
+/* Pattern read ceiling: reads exactly the 16-B chunks the checksum kernel reads for each
+ * descriptor's L3 range (teams of 8 lanes, non-temporal), with no checksum work, and writes
+ * one word per block into d_sink[0..1023].  grid 0 = 8 blocks per CU; grid bit 31 set = walk the
+ * packets in the checksum kernel's unit order instead of grid-consecutively.  Arenas < 4 GiB.
+ * Tooling: prices a workload's frame layout. */
+int vpcsum_pattern_probe_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc,
+                               uint32_t n, uint32_t* d_sink, uint32_t grid, void* stream);
+
 /* Synthetic workload generator (bench / tests): deterministic counter-based splitmix64 bytes,
  * identical to oracle/csum_oracle.c:orc_synth_frame.  workload: see VPCSUM_SYNTH_*. */
 #define VPCSUM_SYNTH_C1_UDP64     1  /* IPv4/UDP L3 50 B                     */

@@ -223,6 +223,16 @@ int vpcsum_read_probe_async(const uint8_t* d_buf, uint64_t bytes, uint32_t* d_si
     return 0;
 }
 
+int vpcsum_pattern_probe_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, uint32_t n,
+                               uint32_t* d_sink, uint32_t grid, void* stream) {
+    if (n == 0) return 0;
+    if (!d_arena || !d_desc || !d_sink) return fail("vpcsum_pattern_probe_async: NULL argument");
+    if (arena_len >= (1ull << 32)) return fail("vpcsum_pattern_probe_async: arena must be < 4 GiB");
+    VPC_CHECK(launch_pattern_probe(d_arena, arena_len, d_desc, n, d_sink, grid, (hipStream_t)stream),
+              "pattern probe launch");
+    return 0;
+}
+
 int vpcsum_synth_async(uint8_t* d_arena, uint64_t arena_len, uint32_t n, uint32_t stride, uint32_t l3_pad,
                        uint32_t workload, uint64_t seed, uint64_t first_index, vpcsum_desc_t* d_desc, void* stream) {
     if (n == 0) return 0;

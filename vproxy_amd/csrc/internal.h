@@ -35,6 +35,8 @@ hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const ui
                               uint8_t* status, hipStream_t stream);
 
 hipError_t launch_read_probe(const uint8_t* buf, uint64_t bytes, uint32_t* sink, uint32_t grid, hipStream_t stream);
+hipError_t launch_pattern_probe(const uint8_t* arena, uint64_t arena_len, const void* desc, uint32_t n, uint32_t* sink,
+                                uint32_t grid, hipStream_t stream);
 
 hipError_t launch_synth(uint8_t* arena, uint64_t arena_len, uint32_t n, uint32_t stride, uint32_t l3_pad,
                         uint32_t workload, uint64_t seed, uint64_t first_index, vpcsum_desc_t* desc,

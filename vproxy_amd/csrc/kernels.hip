@@ -1438,6 +1438,124 @@ hipError_t launch_read_probe(const uint8_t* buf, uint64_t bytes, uint32_t* sink,
     return hipGetLastError();
 }
 
+// Pattern ceiling of a batch: the same 16-B chunk reads as K2's large tier (teams of 8 lanes,
+// 6 non-temporal buffer loads in flight per lane, out-of-range chunks predicated off), and no
+// checksum work.  Grid-stride over packets, one team per packet.
+template <bool PIPE>
+__global__ __launch_bounds__(256) void k_pattern_probe(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                       const uint4* __restrict__ desc, uint32_t n,
+                                                       uint32_t* __restrict__ sink, uint32_t order) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    constexpr int TEAM = 8, U = 6;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
+    const int tl = threadIdx.x & (TEAM - 1);
+    const uint32_t nteams = gridDim.x * (256 / TEAM);
+    uint32_t x = 0;
+    // order 0: the grid's teams walk consecutive packets.  order 1: K2's order (a wave owns 64
+    // consecutive packets, its 8 teams take them 8 at a time; units grid-strided).
+    const uint32_t tpw = 64 / TEAM;
+    const uint32_t wave = (blockIdx.x * 256 + threadIdx.x) >> 6, nwaves = gridDim.x * 4;
+    const uint32_t tw = (threadIdx.x & 63) / TEAM;
+    auto packet = [&](uint32_t i) -> uint32_t {   // i-th packet of this team, ~0u past the end
+        uint32_t p;
+        if (order == 0) {
+            p = (blockIdx.x * 256 + threadIdx.x) / TEAM + i * nteams;
+        } else {
+            const uint32_t unit = wave + (i / 8) * nwaves;
+            if (unit * 64 >= n) return ~0u;
+            p = unit * 64 + (i % 8) * tpw + tw;
+            if (p >= n) return ~1u;   // a hole in a partial unit: skip
+        }
+        return p < n ? p : ~0u;
+    };
+    auto issue = [&](v4u* v, uint32_t boff, int nch, int rr) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = (rr + u) * TEAM + tl;
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange, 0, 2);
+        }
+    };
+    if (!PIPE) {
+        for (uint32_t i = 0;; ++i) {
+            const uint32_t p = packet(i);
+            if (p == ~0u) break;
+            if (p == ~1u) continue;
+            const uint4 d = desc[p];
+            const uint32_t boff = d.x & ~15u;
+            const int nch = (int)(((d.x & 15) + (d.z & 0xffff) + 15) >> 4);
+            for (int rr = 0; rr * TEAM < nch; rr += U) {
+                v4u v[U];
+                issue(v, boff, nch, rr);
+#pragma unroll
+                for (int u = 0; u < U; ++u) x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+            }
+        }
+    } else {
+        // the next trip's loads are issued before the current trip is consumed, so the team
+        // always has U loads per lane in flight (descriptors prefetched one packet ahead)
+        uint32_t i = 0, p = packet(0);
+        while (p == ~1u) p = packet(++i);
+        if (p != ~0u) {
+            uint4 d = desc[p];
+            uint32_t pn = packet(i + 1), in = i + 1;
+            while (pn == ~1u) pn = packet(++in);
+            uint4 dn = pn != ~0u ? desc[pn] : make_uint4(0, 0, 0, 0);
+            uint32_t boff = d.x & ~15u;
+            int nch = (int)(((d.x & 15) + (d.z & 0xffff) + 15) >> 4);
+            int rr = 0;
+            v4u a[U], b[U];
+            issue(a, boff, nch, rr);
+            for (;;) {
+                rr += U;
+                bool last = false;
+                if (rr * TEAM >= nch) {   // next packet
+                    if (pn == ~0u) {
+                        last = true;
+                    } else {
+                        d = dn;
+                        boff = d.x & ~15u;
+                        nch = (int)(((d.x & 15) + (d.z & 0xffff) + 15) >> 4);
+                        rr = 0;
+                        i = in;
+                        pn = packet(i + 1), in = i + 1;
+                        while (pn == ~1u) pn = packet(++in);
+                        if (pn != ~0u) dn = desc[pn];
+                    }
+                }
+                if (!last) issue(b, boff, nch, rr);
+#pragma unroll
+                for (int u = 0; u < U; ++u) x ^= a[u].x ^ a[u].y ^ a[u].z ^ a[u].w;
+                if (last) break;
+#pragma unroll
+                for (int u = 0; u < U; ++u) a[u] = b[u];
+            }
+        }
+    }
+    for (int m = 32; m >= 1; m >>= 1) x ^= __shfl_xor(x, m, 64);
+    if ((threadIdx.x & 63) == 0) atomicXor(&sink[blockIdx.x & 1023], x);
+}
+
+hipError_t launch_pattern_probe(const uint8_t* arena, uint64_t arena_len, const void* desc, uint32_t n, uint32_t* sink,
+                                uint32_t grid, hipStream_t stream) {
+    // tooling: grid bit 31 selects K2's packet order, bit 30 the software-pipelined trip stream
+    const uint32_t order = grid >> 31;
+    const bool pipe = (grid >> 30) & 1;
+    grid &= 0x3fffffffu;
+    if (grid == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        grid = num_cus(dev) * 8;
+    }
+    if (pipe)
+        hipLaunchKernelGGL(k_pattern_probe<true>, dim3(grid), dim3(256), 0, stream, arena, arena_len, (const uint4*)desc,
+                           n, sink, order);
+    else
+        hipLaunchKernelGGL(k_pattern_probe<false>, dim3(grid), dim3(256), 0, stream, arena, arena_len,
+                           (const uint4*)desc, n, sink, order);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------
 // Synthetic workload generator: same bytes as oracle/csum_oracle.c:orc_synth_frame.
 // ------------------------------------------------------------------------------------------

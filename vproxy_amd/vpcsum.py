@@ -32,6 +32,7 @@ NAT4_DTYPE = np.dtype([("src", "u1", 4), ("dst", "u1", 4), ("sport", "u1", 2), (
 EXPORTS = [
     "vpcsum_abi_version", "vpcsum_last_error", "vpcsum_device_count", "vpcsum_set_device",
     "vpcsum_compute_async", "vpcsum_nat4_async", "vpcsum_parse_ether_async", "vpcsum_read_probe_async",
+    "vpcsum_pattern_probe_async",
     "vpcsum_synth_async", "vpcsum_event_create", "vpcsum_event_destroy", "vpcsum_event_record",
     "vpcsum_event_elapsed_ms", "vpcsum_stream_sync", "vpcsum_ctx_create", "vpcsum_ctx_destroy",
     "vpcsum_ctx_register_arena", "vpcsum_ctx_unregister_arena", "vpcsum_ctx_submit", "vpcsum_ctx_wait",
@@ -66,6 +67,7 @@ def _declare(L):
         "vpcsum_nat4_async": ([P, U64, P, P, U32, P, U32, P], I),
         "vpcsum_parse_ether_async": ([P, U64, P, P, U32, U8, P, P, P], I),
         "vpcsum_read_probe_async": ([P, U64, P, U32, P], I),
+        "vpcsum_pattern_probe_async": ([P, U64, P, U32, P, U32, P], I),
         "vpcsum_synth_async": ([P, U64, U32, U32, U32, U32, U64, U64, P, P], I),
         "vpcsum_event_create": ([P], I),
         "vpcsum_event_destroy": ([P], I),
@@ -158,6 +160,13 @@ def nat4(arena, desc, rw, n: int, status=None, nat_mode: int = NAT_RFC1624, stre
 def parse_ether(arena, frame_off, frame_len, n: int, desc, status=None, flags: int = F_IP | F_L4, stream=None):
     _check(lib().vpcsum_parse_ether_async(_ptr(arena), arena.numel(), _ptr(frame_off), _ptr(frame_len), n, flags,
                                           _ptr(desc), _ptr(status), _stream(stream)), "vpcsum_parse_ether_async")
+
+
+def pattern_probe(arena, desc, n: int, sink, grid: int = 0, stream=None):
+    """Read exactly the chunks the checksum kernel reads for `desc`, no checksum work (tooling)."""
+    assert sink.numel() * sink.element_size() >= 4096, "sink needs 1024 words"
+    _check(lib().vpcsum_pattern_probe_async(_ptr(arena), arena.numel(), _ptr(desc), n, _ptr(sink), grid,
+                                            _stream(stream)), "vpcsum_pattern_probe_async")
 
 
 def read_probe(buf, nbytes: int, sink, grid: int = 0, stream=None):
