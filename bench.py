@@ -172,6 +172,19 @@ def main():
     e1.record(stream)
     probe_ms = e0.elapsed_ms(e1) / 10
     read_ceiling = arena.numel() / (probe_ms * 1e-3) / 1e9
+    # pattern ceiling: a read-only kernel over exactly this batch's chunks (no checksum work),
+    # best of 2 and 4 workgroups per CU, in algorithmic bytes like `achieved`
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    pattern_ms = []
+    for bpc in (2, 4):
+        for _ in range(3):
+            V.pattern_probe(arena, d, n, sink, cus * bpc, stream=stream)
+        e0.record(stream)
+        for _ in range(10):
+            V.pattern_probe(arena, d, n, sink, cus * bpc, stream=stream)
+        e1.record(stream)
+        pattern_ms.append(e0.elapsed_ms(e1) / 10)
+    pattern_ceiling = bytes_per_step / (min(pattern_ms) * 1e-3) / 1e9
 
     # correctness on the benchmarked batch: write the sums in place, then verify every packet
     V.compute(arena, d, n, out, status, V.MODE_WRITE, args.team, stream=stream)
@@ -223,6 +236,8 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_step,
                 "kernel_avg_ms": round(kernel_ms, 5),
                 "measured_read_ceiling_GBps": round(read_ceiling, 1),
+                "measured_pattern_ceiling_GBps": round(pattern_ceiling, 1),
+                "frac_of_pattern_ceiling": round(achieved / pattern_ceiling, 4),
             },
             "cpu_baseline": cpu,
         }

@@ -37,10 +37,14 @@ def main(tag):
         d = json_line(os.path.join(G, log))
         if d:
             json.dump(d, open(os.path.join(P, f"{tag}_bench_{wl}.json"), "w"))
-    for name, out in (("natbench.log", "nat_c5"), ("hostpath.log", "hostpath_c2")):
+    for name, out in (("natbench.log", "nat_c5"), ("hostpath.log", "hostpath_c2"),
+                      ("pattern_all.log", "pattern_ceiling"), ("bench_2rank.log", "bench_2rank_1gpu")):
         d = json_line(os.path.join(G, name))
         if d:
             json.dump(d, open(os.path.join(P, f"{tag}_{out}.json"), "w"), indent=1)
+    fl = os.path.join(G, "flush_latency.json")
+    if os.path.exists(fl) and json_line(fl):
+        json.dump(json_line(fl), open(os.path.join(P, f"{tag}_flush_latency.json"), "w"), indent=1)
     for src in sorted(glob.glob(os.path.join(G, "pmc_*"))):
         wl = os.path.basename(src)[4:]
         kern = "k_nat4w" if wl == "nat" else "k_csum"
