@@ -92,10 +92,11 @@ def pmc_traffic(workload: str, team: int):
     if team != 0:
         return None, None
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{workload}", "summary.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    return int(d["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
+    for f in reversed(files):   # newest summary that carries the corrected HBM bytes
+        d = json.load(open(f))
+        if "hbm_bytes_per_launch" in d:
+            return int(d["hbm_bytes_per_launch"]), os.path.relpath(f, REPO)
+    return None, None
 
 
 def main():
@@ -185,6 +186,9 @@ def main():
         e1.record(stream)
         pattern_ms.append(e0.elapsed_ms(e1) / 10)
     pattern_ceiling = bytes_per_step / (min(pattern_ms) * 1e-3) / 1e9
+    if desc_np["l3_len"].mean() < 512:
+        # its 8-lane teams idle on small packets: no ceiling there (measured_read_ceiling is)
+        pattern_ceiling = None
 
     # correctness on the benchmarked batch: write the sums in place, then verify every packet
     V.compute(arena, d, n, out, status, V.MODE_WRITE, args.team, stream=stream)
@@ -236,8 +240,8 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_step,
                 "kernel_avg_ms": round(kernel_ms, 5),
                 "measured_read_ceiling_GBps": round(read_ceiling, 1),
-                "measured_pattern_ceiling_GBps": round(pattern_ceiling, 1),
-                "frac_of_pattern_ceiling": round(achieved / pattern_ceiling, 4),
+                "measured_pattern_ceiling_GBps": round(pattern_ceiling, 1) if pattern_ceiling else None,
+                "frac_of_pattern_ceiling": round(achieved / pattern_ceiling, 4) if pattern_ceiling else None,
             },
             "cpu_baseline": cpu,
         }
