@@ -401,7 +401,16 @@ def test_context_pipeline(V, orc):
     ctx.register(out)
     ctx.pipeline(arena, stride, 1504, desc, out, chunks=8)
     assert np.array_equal(out, want)
+    # a descriptor outside the copied part of its chunk's frames is refused, not read
+    d2 = desc.copy()
+    ctx.register(d2)   # registered until close: keep the array alive
+    for i, bad in ((3000, 0), (7, 1600), (19999, n * stride)):
+        d2[:] = desc
+        d2["l3_off"][i] = bad
+        with pytest.raises(V.VpcsumError, match="outside the copied frames"):
+            ctx.pipeline(arena, stride, 1504, d2, out, chunks=8)
     ctx.close()
+    del d2
 
 
 def test_full_size_c2_properties(V, orc):

@@ -493,9 +493,9 @@ static int slot_finish(vpcsum_ctx* c, Slot& s) {
         // place the GPU results into the caller's frames (big endian, as ByteArray.int16)
         for (uint32_t i = 0; i < s.n; ++i) {
             const vpcsum_desc_t& d = s.user_desc[i];
-            if (s.h_status[i] & VPCSUM_S_BAD_DESC) continue;
+            if (res_status[i] & VPCSUM_S_BAD_DESC) continue;
             uint8_t* l3 = s.user_arena + d.l3_off;
-            const uint32_t w = s.h_out[i];
+            const uint32_t w = res_out[i];
             if (d.flags & VPCSUM_F_IP) { l3[10] = (uint8_t)(w >> 8); l3[11] = (uint8_t)w; }
             if (d.flags & (VPCSUM_F_L4 | VPCSUM_F_L4P)) {
                 const int fld = d.l4_proto == 6 ? 16 : d.l4_proto == 17 ? 6 : 2;
@@ -716,6 +716,16 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint
     const bool desc_pinned = is_registered(c, (const uint8_t*)h_desc, (uint64_t)n * sizeof(vpcsum_desc_t));
     const bool out_pinned = is_registered(c, (const uint8_t*)h_out, (uint64_t)n * 4);
     if (!desc_pinned || !out_pinned) return fail("vpcsum_ctx_pipeline: descriptors and out must be registered");
+    // each chunk's device view starts at frame i0, and only the first copy_bytes of every frame
+    // are copied: a descriptor must lie inside the copied part of a frame of its own chunk
+    // (below the view it would address memory before the device slot)
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t i0 = (uint64_t)(i / per) * per;
+        const uint64_t off = h_desc[i].l3_off;
+        if (off < i0 * stride || off >= (uint64_t)n * stride || off % stride + h_desc[i].l3_len > copy_bytes)
+            return fail("vpcsum_ctx_pipeline: descriptor %u [%llu, +%u) outside the copied frames", i,
+                        (unsigned long long)off, (unsigned)h_desc[i].l3_len);
+    }
     for (uint32_t k = 0; k < chunks; ++k) {
         const uint32_t i0 = k * per;
         if (i0 >= n) break;

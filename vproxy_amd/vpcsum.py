@@ -212,12 +212,18 @@ class Context:
         h = ctypes.c_void_p()
         _check(lib().vpcsum_ctx_create(device, max_arena, max_pkts, ctypes.byref(h)), "vpcsum_ctx_create")
         self.h = h.value
+        # numpy buffers the library holds raw pointers to: registered arrays (until unregister /
+        # close) and the buffers of the batch in flight on each of the context's two slots
+        self._pinned = {}
+        self._inflight = {}
 
     def register(self, arr: np.ndarray):
         _check(lib().vpcsum_ctx_register_arena(self.h, arr.ctypes.data, arr.nbytes), "vpcsum_ctx_register_arena")
+        self._pinned[arr.ctypes.data] = arr
 
     def unregister(self, arr: np.ndarray):
         _check(lib().vpcsum_ctx_unregister_arena(self.h, arr.ctypes.data), "vpcsum_ctx_unregister_arena")
+        self._pinned.pop(arr.ctypes.data, None)
 
     def submit(self, arena: np.ndarray, desc: np.ndarray, out: np.ndarray, status: np.ndarray | None = None,
                mode: int = MODE_COMPUTE) -> int:
@@ -225,6 +231,7 @@ class Context:
         _check(lib().vpcsum_ctx_submit(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data, len(desc),
                                        out.ctypes.data, None if status is None else status.ctypes.data, mode,
                                        ctypes.byref(t)), "vpcsum_ctx_submit")
+        self._inflight[t.value & 1] = (arena, desc, out, status)
         return t.value
 
     def wait(self, ticket: int):
@@ -269,6 +276,8 @@ class Context:
         if self.h:
             lib().vpcsum_ctx_destroy(self.h)
             self.h = None
+            self._pinned.clear()
+            self._inflight.clear()
 
     def __del__(self):
         try:
