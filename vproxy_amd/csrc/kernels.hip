@@ -90,6 +90,11 @@ constexpr int kDefaultUnroll = 6;
 // (64 B incl. alignment) are streamed by 2-lane teams, 32 packets per iteration.
 constexpr int kSmallTeam = 2;
 constexpr int kSmallUnroll = 2;
+// Large-tier slot rotation of the default kernel: wave w starts its unit at slot (9 w) mod the
+// tier size.  Units are 64 packets, a power-of-two stride apart (128 KB at a 2-KB frame stride);
+// without it, all waves read the same offset within their units at the same moment, and the
+// HBM channel/bank mapping aliases those addresses: C2 -4%.
+constexpr int kDefaultRot = -9;
 
 // Sum over the TEAM lanes of a team (aligned lane groups; every lane gets the total).  Teams of
 // up to 16 lanes reduce with DPP lane swizzles inside a row (xor 1, xor 2 by quad_perm, then
@@ -471,17 +476,30 @@ __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, ui
 
 // Phase B of K2 for one tier: slots [s_begin, s_end) streamed by teams of TEAM lanes, 64/TEAM
 // packets per iteration; each team leaves {l4, ip, pseudo, stored} sums in its slot's q0.
-template <int TEAM, int U, bool VERIFY, bool NT>
+template <int TEAM, int U, bool VERIFY, bool NT, bool SLOTROT = false>
 __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, uint4 (*slots)[4], int lane,
-                                            int s_begin, int s_end) {
+                                            int s_begin, int s_end, uint32_t rot = 0) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     constexpr int PPI = 64 / TEAM;
     const int tl = lane & (TEAM - 1);
     const int tid = lane / TEAM;
+    // rot: this wave starts at iteration rot (mod the count), so that waves whose units are a
+    // power-of-two stride apart do not read the same offsets within their units at once
+    const int nit = (s_end - s_begin + PPI - 1) / PPI;
+    const int range = s_end - s_begin;
+    const int r0 = nit > 0 ? (int)(rot % (uint32_t)(SLOTROT ? range : nit)) : 0;
 #pragma unroll 1
-    for (int base = s_begin; base < s_end; base += PPI) {
-        const int sidx = base + tid;
-        const bool act = sidx < s_end;
+    for (int it = 0; it < nit; ++it) {
+        int sidx;
+        bool act;
+        if (SLOTROT) {   // rotation by slots: the wave's first packet is slot r0
+            const int q = it * PPI + tid;
+            act = q < range;
+            sidx = s_begin + (q + r0 < range ? q + r0 : q + r0 - range);
+        } else {
+            sidx = s_begin + (it + r0 < nit ? it + r0 : it + r0 - nit) * PPI + tid;
+            act = sidx < s_end;
+        }
         uint4* sl = slots[act ? sidx : 0];
         uint4 a = sl[0];
         if (!act) a = make_uint4(0, 0, 0, 0);
@@ -533,7 +551,9 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
 
 // K2 body for workgroup `blk` of a grid of `gdim` workgroups (k_csum_d: the launch grid;
 // k_csum_service: the persistent service grid, once per batch).
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL>
+// ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
+// ROT > 0 rotates whole iterations (64 / TEAM packets), ROT < 0 single slots.
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0>
 __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -625,7 +645,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         }
         const int r0 = (int)(off & 15);
         int key = 0;
-        int n_small = 0;
+        int n_small = 0, n_cls = 0;   // n_cls: distinct cost classes in the large tier
         {
             PktPlan pl;
             pl.r0 = r0;
@@ -681,6 +701,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                 if (key == b)
                     rank = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
                 cnt += (uint32_t)__popcll(m);
+                if (b >= 2 && m) ++n_cls;
                 if (b == 1) n_small = (int)cnt;   // keys 0 and 1 go to the small tier
             }
             key = (int)rank;   // from here on: this packet's slot
@@ -698,7 +719,10 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         // ---- phase B: teams stream the packets in slot order ----
         if (TS > 0) {
             stream_tier<(TS > 0 ? TS : 1), US, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, n_small);
-            stream_tier<TEAM, U, VERIFY, NT>(rsrc, s_slot[wid], lane, n_small, 64);
+            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0)>(rsrc, s_slot[wid], lane, n_small, 64,
+                                             // rotated only when the tier is one cost class: in a
+                                             // sorted mixed tier the wrap would pair unlike sizes
+                                             (ROT && n_cls == 1) ? (blk * 4u + (uint32_t)wid) * (uint32_t)(ROT < 0 ? -ROT : ROT) : 0u);
         } else {
             stream_tier<TEAM, U, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, 64);
         }
@@ -763,13 +787,13 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     }
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
                                                 uint8_t* __restrict__ arena_w, uint32_t low_grid) {
-    k2_run<TEAM, U, TS, US, VERIFY, NT, IL>(arena, arena_len, desc, n, out, status, flags_override, arena_w, low_grid,
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT>(arena, arena_len, desc, n, out, status, flags_override, arena_w, low_grid,
                                             blockIdx.x, gridDim.x);
 }
 
@@ -879,7 +903,7 @@ static uint32_t default_low_grid() {
     return (uint32_t)num_cus(dev) * 2u;
 }
 
-template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, bool adapt, hipStream_t stream) {
@@ -896,7 +920,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE, IL>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
+    hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
                        (const uint4*)desc, n, out, status, flags_override, arena_w, low_grid)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -943,7 +967,8 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 54: return launch_d<8, 4, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 58: return launch_d<8, 12, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 62: return launch_d<8, 6, 2, 2, 1, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
-        case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 66: return launch_d<8, 6, 2, 2, 1, 0, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         default: return hipErrorInvalidValue;   // unknown kernel variant id
     }
 #undef VPC_T
