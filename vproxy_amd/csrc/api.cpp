@@ -9,10 +9,12 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <chrono>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -109,7 +111,8 @@ constexpr uint32_t kSvcBatchMax = 512;
 struct Service {
     vpcsum::SvcMailbox* mb = nullptr;    // host-pinned, coherent (uncached on the GPU), mapped
     vpcsum::SvcMailbox* dmb = nullptr;   // its device address
-    uint32_t* ctr = nullptr;             // device: workgroups finished with the current batch
+    uint32_t* ctr = nullptr;             // device: workgroups finished with the current batch,
+                                         // then (8-B aligned, ctr + 2) the command relay
     hipStream_t stream = nullptr;
     // the service's own descriptor / result buffers (pinned, coherent, mapped) and their device
     // addresses: the same for every batch, so the parameter block rarely changes
@@ -124,6 +127,10 @@ struct Service {
     uint32_t posted = 0;                 // last batch published (seq)
     uint64_t idle_ticks = 0;             // 100 MHz ticks
     bool on = false;
+#ifdef VPCSUM_SVC_STAMPS
+    std::chrono::steady_clock::time_point t_post;
+    uint32_t t_n = 0;
+#endif
 };
 
 struct vpcsum_ctx {
@@ -330,7 +337,7 @@ int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
         (e = hipHostGetDevicePointer((void**)&v.dh_desc, v.h_desc, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&v.dh_out, v.h_out, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&v.dh_status, v.h_status, 0)) != hipSuccess ||
-        (e = hipMalloc((void**)&v.ctr, sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc((void**)&v.ctr, 16)) != hipSuccess ||   // counter + command relay
         (e = hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking)) != hipSuccess) {
         svc_free(c);
         return hipfail(e, "vpcsum_ctx_set_service allocation");
@@ -454,7 +461,7 @@ static uint32_t svc_done(const Service& v) { return __atomic_load_n(&v.mb->done,
 // of this context runs (stream idle), so the finished-wave counter can be cleared first.
 static int svc_launch(vpcsum_ctx* c, uint32_t seen) {
     Service& v = c->svc;
-    VPC_CHECK(hipMemsetAsync(v.ctr, 0, sizeof(uint32_t), v.stream), "service counter reset");
+    VPC_CHECK(hipMemsetAsync(v.ctr, 0, 16, v.stream), "service counter / relay reset");
     VPC_CHECK(launch_service(v.dmb, v.ctr, seen, v.idle_ticks, v.stream), "service launch");
     ++c->svc_launches;
     return 0;
@@ -463,6 +470,24 @@ static int svc_launch(vpcsum_ctx* c, uint32_t seen) {
 // Wait until the service has completed batch `seq`.  A grid that left on its idle timeout while
 // the batch was being posted may have done part of it: once the stream is idle the batch is run
 // again from the start by a fresh grid (the sums do not read the fields they write).
+#ifdef VPCSUM_SVC_STAMPS
+// tooling build: per-batch durations of the service's steps (ns), medians per batch size at exit
+static std::map<uint32_t, std::vector<uint64_t>> g_stamp_d[7];
+static void stamps_print() {
+    static const char* name[7] = {"host_post_to_done_seen_ns", "wg0_params_ns", "wg0_k1_ns", "wg0_release_ns",
+                                  "wg0_atomic_ns", "wg0_seen_to_done_store_ns", "last_wg_seen_after_wg0_ns"};
+    for (auto& kv : g_stamp_d[0]) {
+        fprintf(stderr, "{\"n\": %u", kv.first);
+        for (int i = 0; i < 7; ++i) {
+            auto v = g_stamp_d[i][kv.first];
+            std::sort(v.begin(), v.end());
+            fprintf(stderr, ", \"%s\": %llu", name[i], (unsigned long long)v[v.size() / 2]);
+        }
+        fprintf(stderr, "}\n");
+    }
+}
+#endif
+
 static int svc_wait(vpcsum_ctx* c, uint32_t seq) {
     Service& v = c->svc;
     const auto t0 = std::chrono::steady_clock::now();
@@ -475,6 +500,20 @@ static int svc_wait(vpcsum_ctx* c, uint32_t seq) {
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
             return fail("vpcsum service: batch %u not completed within 10 s", seq);
     }
+#ifdef VPCSUM_SVC_STAMPS
+    {
+        static bool reg = false;
+        if (!reg) { reg = true; atexit(stamps_print); }
+        const uint64_t* s = (const uint64_t*)v.mb->stamp;
+        const uint64_t s0 = s[0];
+        const uint32_t n = v.t_n;
+        g_stamp_d[0][n].push_back((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+            std::chrono::steady_clock::now() - v.t_post).count());
+        for (int i = 1; i <= 4; ++i) g_stamp_d[i][n].push_back((s[i] - s[i - 1]) * 10);
+        g_stamp_d[5][n].push_back((s[5] - s0) * 10);
+        g_stamp_d[6][n].push_back((s[6] - s0) * 10);
+    }
+#endif
     return 0;
 }
 
@@ -563,6 +602,10 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
             }
             const uint32_t seq = v.posted + 1 ? v.posted + 1 : 1;
             cmd |= seq | ((uint64_t)n << 32) | ((mode & VPCSUM_MODE_VERIFY) ? kSvcVerify : 0);
+#ifdef VPCSUM_SVC_STAMPS
+            v.t_post = std::chrono::steady_clock::now();
+            v.t_n = n;
+#endif
             __atomic_store_n(&mb->cmd, cmd, __ATOMIC_RELEASE);
             v.posted = seq;
             ++c->svc_batches;

@@ -20,6 +20,8 @@ struct alignas(64) SvcMailbox {
     uint64_t cmd;        // host: seq (bits 0..31, 0 = none yet) | n (32..59) | kSvcStop | kSvcVerify | kSvcParams
     uint64_t arena, arena_len, arena_w, desc, out, status, rsv;   // device addresses; read when kSvcParams
     alignas(64) uint32_t done;   // device: last completed batch
+    uint32_t pad_;
+    uint64_t stamp[7];           // VPCSUM_SVC_STAMPS builds only: s_memrealtime per batch step
 };
 static_assert(sizeof(uint64_t) * 8 == 64, "SvcMailbox parameter block: one 64-B line");
 constexpr uint64_t kSvcStop = 1ull << 61, kSvcVerify = 1ull << 62, kSvcParams = 1ull << 63;

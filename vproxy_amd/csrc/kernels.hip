@@ -801,13 +801,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // Low-latency service: the checksum on a persistent grid of kServiceGrid workgroups that polls
 // a host mailbox (internal.h SvcMailbox) instead of being launched per batch, for the small
 // flushes of Iface.completeTx (XDPIface.java:227-243) on a registered umem, where a kernel
-// launch plus an event wait cost more than the work.  Thread 0 of each workgroup polls the
-// command word at system scope; a new batch is processed by all workgroups (one packet per
-// wave, grid-stride); each workgroup releases its results at system scope and bumps a device
-// counter, and the workgroup that completes the count resets it and publishes `done`.  The grid
-// leaves on kSvcStop or after idle_ticks (100 MHz s_memrealtime) without a batch; the host
-// relaunches it on demand and re-runs a batch that a leaving grid left unfinished (idempotent:
-// checksum fields are excluded from the sums they hold).
+// launch plus an event wait cost more than the work.  Thread 0 of workgroup 0 alone polls the
+// command word at system scope and relays it to the other workgroups through a device-memory
+// word (32 pollers of one host line slowed each poll's round trip 2-4x, tools/bar_probe.cpp).
+// A batch is processed by the workgroups that own a packet (one packet per wave, grid-stride);
+// each of them releases its results at system scope and bumps a device counter, and the one
+// that completes the count resets it and publishes `done`.  The grid leaves on kSvcStop or
+// after idle_ticks (100 MHz s_memrealtime) without a batch (workgroup 0 relays the stop); the
+// host relaunches it on demand and re-runs a batch that a leaving grid left unfinished
+// (idempotent: checksum fields are excluded from the sums they hold).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* __restrict__ ctr, uint32_t seen,
                                                       uint64_t idle_ticks) {
@@ -815,25 +817,49 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
     // in LDS across batches: arena, arena_len, arena_w, desc, out, status
     __shared__ uint64_t s_par[6];
     __shared__ uint64_t s_cmd;
+#ifdef VPCSUM_SVC_STAMPS
+    __shared__ uint64_t s_ts;
+#endif
     bool have_par = false;
+    uint64_t* relay = reinterpret_cast<uint64_t*>(ctr + 2);   // zeroed with the counter at launch
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         if (threadIdx.x == 0) {
             uint64_t cmd = 0;
-            for (;;) {   // one 8-B PCIe read per poll
-                const uint64_t w = __hip_atomic_load(&mb->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (w & kSvcStop) break;
-                if ((uint32_t)w != seen) { cmd = w; break; }
-                const uint64_t idle = __builtin_amdgcn_s_memrealtime() - t0;
-                if (idle > idle_ticks) break;
-                // back off after 50 us without a batch: ~1 us more latency, far fewer PCIe reads
-                if (idle > 5000) __builtin_amdgcn_s_sleep(40);
-                else __builtin_amdgcn_s_sleep(1);
+            if (blockIdx.x == 0) {
+                for (;;) {   // the grid's only reader of the host mailbox: one 8-B PCIe read per poll
+                    const uint64_t w = __hip_atomic_load(&mb->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (w & kSvcStop) break;
+                    if ((uint32_t)w != seen) { cmd = w; break; }
+                    const uint64_t idle = __builtin_amdgcn_s_memrealtime() - t0;
+                    if (idle > idle_ticks) break;
+                    // back off after 50 us without a batch: ~1 us more latency, far fewer PCIe reads
+                    if (idle > 5000) __builtin_amdgcn_s_sleep(40);
+                    else __builtin_amdgcn_s_sleep(1);
+                }
+                // to the other workgroups: the command, or a stop when the grid leaves
+                __hip_atomic_store(relay, cmd ? cmd : (kSvcStop | seen), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                for (;;) {   // the relay in device memory
+                    const uint64_t w = __hip_atomic_load(relay, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    if (w & kSvcStop) break;
+                    if (w && (uint32_t)w != seen) { cmd = w; break; }
+                    // workgroup 0 relays a stop before it leaves; this bound only guards the grid
+                    // against a relay that never comes
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * idle_ticks + 100000) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
             }
+#ifdef VPCSUM_SVC_STAMPS
+            const uint64_t ts_seen = __builtin_amdgcn_s_memrealtime();
+            if (blockIdx.x == 0) mb->stamp[0] = ts_seen;
+            s_ts = ts_seen;
+#endif
             // acquire at system scope: the frames, descriptors and parameters the host wrote
             // before the command word are read fresh (no kernel boundary invalidates caches here)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            if (cmd && ((cmd & kSvcParams) || !have_par)) {
+            const uint32_t next = seen + 1 ? seen + 1 : 1;   // the host's sequence skips 0
+            if (cmd && ((cmd & kSvcParams) || !have_par || (uint32_t)cmd != next)) {
                 // the 64-B block in one round trip: four independent 16-B loads
                 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
                 const v4u* pb = (const v4u*)mb;
@@ -848,6 +874,9 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                 s_par[5] = (uint64_t)q[3].x | ((uint64_t)q[3].y << 32);   // status
             }
             s_cmd = cmd;
+#ifdef VPCSUM_SVC_STAMPS
+            if (blockIdx.x == 0) mb->stamp[1] = __builtin_amdgcn_s_memrealtime();
+#endif
         }
         __syncthreads();
         const uint64_t cmd = s_cmd;
@@ -861,6 +890,10 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         if (cmd == 0) return;
         have_par = true;
         const uint32_t n = (uint32_t)(cmd >> 32) & kSvcMaxPkts;
+        // only the workgroups that own a packet take part (packet p goes to wave p mod the grid's
+        // waves, workgroup (p / 4) mod grid): a flush of a few frames waits for no relay
+        const uint32_t nwg = max(1u, min(gridDim.x, (n + 3u) / 4u));
+        if (blockIdx.x < nwg) {
         // one wave per packet: a small flush is a few PCIe round trips deep (descriptor, frame
         // bytes, results) instead of K2's per-unit iterations, which a latency of ~3 us per
         // round trip would serialize
@@ -869,15 +902,30 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         else
             k1_run<64, 4, false, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
         // the workgroup's stores are complete (barrier); thread 0 releases them system-wide and
-        // counts the workgroup; the last workgroup of the grid publishes `done`
+        // counts the workgroup; the last participating workgroup publishes `done`
         __syncthreads();
         if (threadIdx.x == 0) {
+#ifdef VPCSUM_SVC_STAMPS
+            if (blockIdx.x == 0) mb->stamp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+#ifdef VPCSUM_SVC_STAMPS
+            if (blockIdx.x == 0) mb->stamp[3] = __builtin_amdgcn_s_memrealtime();
+#endif
             const uint32_t d = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-            if (d + 1 == gridDim.x) {
+#ifdef VPCSUM_SVC_STAMPS
+            if (blockIdx.x == 0) mb->stamp[4] = __builtin_amdgcn_s_memrealtime();
+#endif
+            if (d + 1 == nwg) {
+#ifdef VPCSUM_SVC_STAMPS
+                mb->stamp[5] = __builtin_amdgcn_s_memrealtime();
+                mb->stamp[6] = s_ts;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+#endif
                 __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&mb->done, (uint32_t)cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
+        }
         }
         seen = (uint32_t)cmd;
         t0 = __builtin_amdgcn_s_memrealtime();
