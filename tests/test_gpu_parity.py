@@ -684,6 +684,40 @@ def test_service_flushes(V, orc, idle_us):
     ctx.close()
 
 
+@pytest.mark.parametrize("idle_us", [20000, 30])
+def test_service_inline_flushes(V, orc, idle_us):
+    """Flushes of 1..3 frames take their descriptors from the command's mailbox line (tagged
+    with the batch's low sequence byte); 4-frame flushes interleave and read the descriptor
+    buffer.  600 flushes wrap the tag byte twice; descriptors include rejected ones (FUZZ), and
+    consecutive flushes reuse the same inline slots with different descriptors and modes."""
+    n_all, stride = 128, 9216          # frames must not overlap: WRITE mode stores into them
+    a, d = orc.synth(n_all, stride, 14, O.SYNTH_FUZZ, O.SEED, 77 + idle_us)
+    arena = np.zeros(a.size + 4096, np.uint8)
+    arena[:a.size] = a
+    ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=n_all)
+    ctx.register(arena)
+    ctx.set_service(idle_us)
+    rng = np.random.default_rng(idle_us + 1)
+    iters = 600
+    for it in range(iters):
+        b = 4 if it % 7 == 3 else int(rng.integers(1, 4))
+        idx = rng.choice(n_all, size=b, replace=False)
+        dsc = d[idx].copy()
+        mode = (O.MODE_COMPUTE, O.MODE_VERIFY, O.MODE_WRITE)[int(rng.integers(0, 3))]
+        want_arena = arena.copy()
+        want_out, want_st = orc.process(want_arena, dsc, mode & O.MODE_VERIFY, write=bool(mode & O.MODE_WRITE))
+        out = np.zeros(b, np.uint32)
+        st = np.zeros(b, np.uint8)
+        ctx.wait(ctx.submit(arena, dsc, out, st, mode))
+        assert np.array_equal(out, want_out), it
+        assert np.array_equal(st, want_st), it
+        assert np.array_equal(arena, want_arena), it
+        if idle_us < 100 and it % 5 == 0:
+            _busy_us(int(rng.integers(0, 3 * idle_us)))
+    assert ctx.stats()["service_batches"] == iters
+    ctx.close()
+
+
 def test_service_egress_batch(V, orc):
     """EgressBatch with the service: same frames as Java's full recompute after TTL rewrites."""
     from vproxy_amd import vswitch as S

@@ -51,15 +51,19 @@ int main(int argc, char** argv) {
     }
     printf("{");
     const char* sep = "";
-    for (int svc = 0; svc < 2; ++svc) {
+    // pass 2: the service with descriptors read from its buffer only (no inline descriptors in
+    // the command line), for an A/B on the same box
+    for (int svc = 0; svc < 3; ++svc) {
+        if (svc == 2) setenv("VPCSUM_SVC_INLINE", "0", 1);
         if (vpcsum_ctx_set_service(ctx, svc ? 200000 : 0)) {
             fprintf(stderr, "service: %s\n", vpcsum_last_error());
             return 1;
         }
-        printf("%s\"%s\": {", sep, svc ? "service" : "launch");
+        printf("%s\"%s\": {", sep, svc == 2 ? "service_no_inline" : svc ? "service" : "launch");
         sep = ", ";
         const char* sep2 = "";
-        for (uint32_t b : {1u, 32u, 128u, 1024u, 8192u}) {
+        for (uint32_t b : {1u, 3u, 4u, 32u, 128u, 1024u, 8192u}) {
+            if (svc == 2 && b > 4) break;
             std::vector<double> us;
             for (int it = 0; it < iters + 20; ++it) {
                 uint64_t t = 0;

@@ -127,6 +127,8 @@ struct Service {
     uint32_t posted = 0;                 // last batch published (seq)
     uint64_t idle_ticks = 0;             // 100 MHz ticks
     bool on = false;
+    bool inline_desc = true;             // descriptors of <= kSvcInlineDesc frames ride in the command line
+                                         // (VPCSUM_SVC_INLINE=0 turns it off: A/B tooling)
 #ifdef VPCSUM_SVC_STAMPS
     std::chrono::steady_clock::time_point t_post;
     uint32_t t_n = 0;
@@ -347,6 +349,8 @@ int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
     v.mb->out = (uint64_t)(uintptr_t)v.dh_out;
     v.mb->status = (uint64_t)(uintptr_t)v.dh_status;
     v.idle_ticks = (uint64_t)idle_us * 100u;   // s_memrealtime runs at 100 MHz
+    const char* inl = getenv("VPCSUM_SVC_INLINE");
+    v.inline_desc = !(inl && inl[0] == '0');
     v.on = true;
     return 0;
 }
@@ -601,7 +605,22 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
                 cmd |= kSvcParams;
             }
             const uint32_t seq = v.posted + 1 ? v.posted + 1 : 1;
-            cmd |= seq | ((uint64_t)n << 32) | ((mode & VPCSUM_MODE_VERIFY) ? kSvcVerify : 0);
+            // the first descriptors ride in the command's line, tagged with the batch.  All of
+            // them are rewritten for every batch, so a stale one always carries the previous
+            // batch's tag; the high word (with the tag) is stored after the low one.
+            for (int k = 0; k < kSvcInlineDesc; ++k) {
+                vpcsum_desc_t d;
+                if ((uint32_t)k < n) memcpy(&d, &h_desc[k], sizeof(d));
+                else memset(&d, 0, sizeof(d));
+                d.rsv = (uint8_t)seq;
+                uint64_t w[2];
+                memcpy(w, &d, sizeof(w));
+                uint64_t* dst = reinterpret_cast<uint64_t*>(&mb->idesc[k]);
+                __atomic_store_n(&dst[0], w[0], __ATOMIC_RELAXED);
+                __atomic_store_n(&dst[1], w[1], __ATOMIC_RELEASE);
+            }
+            cmd |= seq | ((uint64_t)n << 32) | ((mode & VPCSUM_MODE_VERIFY) ? kSvcVerify : 0) |
+                   (v.inline_desc && n <= (uint32_t)kSvcInlineDesc ? kSvcInline : 0);
 #ifdef VPCSUM_SVC_STAMPS
             v.t_post = std::chrono::steady_clock::now();
             v.t_n = n;

@@ -1,6 +1,7 @@
 // Internal launch interface between the C-ABI layer (api.cpp) and the kernels (kernels.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include "vpcsum.h"
 
@@ -16,15 +17,24 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
 // device-mapped, uncached mailbox instead of being launched per batch.  The host writes the
 // batch's descriptors into the service's own pinned buffers, the parameter block when it
 // changed, then the command word; the grid writes `done` = seq when the batch is finished.
+// The command word shares its 64-B line with the first kSvcInlineDesc descriptors of every
+// batch, each tagged with the batch sequence (low byte, in the descriptor's rsv byte): the
+// poller reads the whole line in one request, so a flush of up to kSvcInlineDesc frames needs
+// no separate descriptor read over PCIe.
+constexpr int kSvcInlineDesc = 3;
 struct alignas(64) SvcMailbox {
-    uint64_t cmd;        // host: seq (bits 0..31, 0 = none yet) | n (32..59) | kSvcStop | kSvcVerify | kSvcParams
-    uint64_t arena, arena_len, arena_w, desc, out, status, rsv;   // device addresses; read when kSvcParams
+    uint64_t cmd;        // host: seq (bits 0..31, 0 = none yet) | n (32..59) | kSvcInline | kSvcStop | kSvcVerify | kSvcParams
+    uint64_t rsv0;
+    vpcsum_desc_t idesc[kSvcInlineDesc];   // host: descriptors 0..2 of the batch, rsv = (uint8_t)seq
+    alignas(64) uint64_t arena;   // line 1, device addresses, read when kSvcParams: arena, then
+    uint64_t arena_len, arena_w, desc, out, status, rsv[2];
     alignas(64) uint32_t done;   // device: last completed batch
     uint32_t pad_;
     uint64_t stamp[7];           // VPCSUM_SVC_STAMPS builds only: s_memrealtime per batch step
 };
-static_assert(sizeof(uint64_t) * 8 == 64, "SvcMailbox parameter block: one 64-B line");
-constexpr uint64_t kSvcStop = 1ull << 61, kSvcVerify = 1ull << 62, kSvcParams = 1ull << 63;
+static_assert(sizeof(vpcsum_desc_t) * kSvcInlineDesc + 16 == 64, "SvcMailbox command line: one 64-B line");
+static_assert(offsetof(SvcMailbox, arena) == 64 && offsetof(SvcMailbox, done) == 128, "SvcMailbox line layout");
+constexpr uint64_t kSvcInline = 1ull << 60, kSvcStop = 1ull << 61, kSvcVerify = 1ull << 62, kSvcParams = 1ull << 63;
 constexpr uint32_t kSvcMaxPkts = (1u << 28) - 1;
 constexpr int kServiceGrid = 32;   // workgroups: 4 waves each, one packet per wave and round
 hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream);

@@ -817,6 +817,8 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
     // in LDS across batches: arena, arena_len, arena_w, desc, out, status
     __shared__ uint64_t s_par[6];
     __shared__ uint64_t s_cmd;
+    __shared__ uint4 s_idesc[kSvcInlineDesc];   // workgroup 0: the inline descriptors of the batch
+    __shared__ uint32_t s_inl;
 #ifdef VPCSUM_SVC_STAMPS
     __shared__ uint64_t s_ts;
 #endif
@@ -824,32 +826,55 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
     uint64_t* relay = reinterpret_cast<uint64_t*>(ctr + 2);   // zeroed with the counter at launch
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        if (threadIdx.x == 0) {
-            uint64_t cmd = 0;
-            if (blockIdx.x == 0) {
-                for (;;) {   // the grid's only reader of the host mailbox: one 8-B PCIe read per poll
-                    const uint64_t w = __hip_atomic_load(&mb->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint64_t got = 0;
+        if (blockIdx.x == 0) {
+            if (threadIdx.x < 64) {
+                // the grid's only reader of the host mailbox: lanes 0..3 of wave 0 read its first
+                // 64-B line in one request per poll -- the command word and the inline descriptors
+                const int lane = threadIdx.x;
+                u32x4_t q = {0u, 0u, 0u, 0u};
+                const u32x4_t* line = reinterpret_cast<const u32x4_t*>(mb) + (lane & 3);
+                for (;;) {
+                    if (lane < 4)   // system-coherent, uncached; volatile: re-read every poll
+                        asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                                     : "=v"(q) : "v"(line) : "memory");
+                    const uint64_t w = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(q.y) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readfirstlane(q.x);
                     if (w & kSvcStop) break;
-                    if ((uint32_t)w != seen) { cmd = w; break; }
+                    if ((uint32_t)w != seen) { got = w; break; }
                     const uint64_t idle = __builtin_amdgcn_s_memrealtime() - t0;
                     if (idle > idle_ticks) break;
                     // back off after 50 us without a batch: ~1 us more latency, far fewer PCIe reads
                     if (idle > 5000) __builtin_amdgcn_s_sleep(40);
                     else __builtin_amdgcn_s_sleep(1);
                 }
-                // to the other workgroups: the command, or a stop when the grid leaves
-                __hip_atomic_store(relay, cmd ? cmd : (kSvcStop | seen), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                for (;;) {   // the relay in device memory
-                    const uint64_t w = __hip_atomic_load(relay, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                    if (w & kSvcStop) break;
-                    if (w && (uint32_t)w != seen) { cmd = w; break; }
-                    // workgroup 0 relays a stop before it leaves; this bound only guards the grid
-                    // against a relay that never comes
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * idle_ticks + 100000) break;
-                    __builtin_amdgcn_s_sleep(1);
+                // inline descriptors: lane 1 + k holds descriptor k.  They are used only when every
+                // one the batch needs carries this batch's tag; otherwise (a line read that caught
+                // the host mid-write) the batch takes them from the descriptor buffer, which the
+                // host filled before the command word.
+                const uint32_t ni = (uint32_t)(got >> 32) & kSvcMaxPkts;
+                const bool need = (got & kSvcInline) && lane >= 1 && lane <= kSvcInlineDesc && (uint32_t)lane <= ni;
+                const bool ok = need && (q.w >> 24) == (got & 0xffu);
+                const bool all = __ballot(ok) == __ballot(need);
+                if (ok) s_idesc[lane - 1] = make_uint4(q.x, q.y, q.z, q.w);
+                if (lane == 0) {
+                    s_inl = (got & kSvcInline) && all ? 1u : 0u;
+                    // to the other workgroups: the command, or a stop when the grid leaves
+                    __hip_atomic_store(relay, got ? got : (kSvcStop | seen), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
+        } else if (threadIdx.x == 0) {
+            for (;;) {   // the relay in device memory
+                const uint64_t w = __hip_atomic_load(relay, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (w & kSvcStop) break;
+                if (w && (uint32_t)w != seen) { got = w; break; }
+                // workgroup 0 relays a stop before it leaves; this bound only guards the grid
+                // against a relay that never comes
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * idle_ticks + 100000) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (threadIdx.x == 0) {
 #ifdef VPCSUM_SVC_STAMPS
             const uint64_t ts_seen = __builtin_amdgcn_s_memrealtime();
             if (blockIdx.x == 0) mb->stamp[0] = ts_seen;
@@ -859,21 +884,21 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
             // before the command word are read fresh (no kernel boundary invalidates caches here)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             const uint32_t next = seen + 1 ? seen + 1 : 1;   // the host's sequence skips 0
-            if (cmd && ((cmd & kSvcParams) || !have_par || (uint32_t)cmd != next)) {
-                // the 64-B block in one round trip: four independent 16-B loads
+            if (got && ((got & kSvcParams) || !have_par || (uint32_t)got != next)) {
+                // the parameter line in one round trip: three independent 16-B loads
                 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-                const v4u* pb = (const v4u*)mb;
-                v4u q[4];
+                const v4u* pb = (const v4u*)&mb->arena;
+                v4u q[3];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) q[k] = __builtin_nontemporal_load(pb + k);
-                s_par[0] = (uint64_t)q[0].z | ((uint64_t)q[0].w << 32);   // arena
-                s_par[1] = (uint64_t)q[1].x | ((uint64_t)q[1].y << 32);   // arena_len
-                s_par[2] = (uint64_t)q[1].z | ((uint64_t)q[1].w << 32);   // arena_w
-                s_par[3] = (uint64_t)q[2].x | ((uint64_t)q[2].y << 32);   // desc
-                s_par[4] = (uint64_t)q[2].z | ((uint64_t)q[2].w << 32);   // out
-                s_par[5] = (uint64_t)q[3].x | ((uint64_t)q[3].y << 32);   // status
+                for (int k = 0; k < 3; ++k) q[k] = __builtin_nontemporal_load(pb + k);
+                s_par[0] = (uint64_t)q[0].x | ((uint64_t)q[0].y << 32);   // arena
+                s_par[1] = (uint64_t)q[0].z | ((uint64_t)q[0].w << 32);   // arena_len
+                s_par[2] = (uint64_t)q[1].x | ((uint64_t)q[1].y << 32);   // arena_w
+                s_par[3] = (uint64_t)q[1].z | ((uint64_t)q[1].w << 32);   // desc
+                s_par[4] = (uint64_t)q[2].x | ((uint64_t)q[2].y << 32);   // out
+                s_par[5] = (uint64_t)q[2].z | ((uint64_t)q[2].w << 32);   // status
             }
-            s_cmd = cmd;
+            s_cmd = got;
 #ifdef VPCSUM_SVC_STAMPS
             if (blockIdx.x == 0) mb->stamp[1] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -883,7 +908,9 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         const uint8_t* arena = (const uint8_t*)s_par[0];
         const uint64_t alen = s_par[1];
         uint8_t* arena_w = (uint8_t*)s_par[2];
-        const uint4* desc = (const uint4*)s_par[3];
+        // a batch of up to kSvcInlineDesc frames runs on workgroup 0 alone (below), from the
+        // descriptors that came with the command
+        const uint4* desc = (blockIdx.x == 0 && s_inl) ? (const uint4*)s_idesc : (const uint4*)s_par[3];
         uint32_t* out = (uint32_t*)s_par[4];
         uint8_t* status = (uint8_t*)s_par[5];
         __syncthreads();   // s_cmd / s_par are rewritten next round
@@ -912,7 +939,8 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
 #ifdef VPCSUM_SVC_STAMPS
             if (blockIdx.x == 0) mb->stamp[3] = __builtin_amdgcn_s_memrealtime();
 #endif
-            const uint32_t d = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            // a batch of one workgroup (up to 4 frames) publishes without the device counter
+            const uint32_t d = nwg == 1 ? 0u : __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef VPCSUM_SVC_STAMPS
             if (blockIdx.x == 0) mb->stamp[4] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -922,7 +950,7 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                 mb->stamp[6] = s_ts;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 #endif
-                __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (nwg > 1) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&mb->done, (uint32_t)cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
