@@ -51,19 +51,22 @@ int main(int argc, char** argv) {
     }
     printf("{");
     const char* sep = "";
-    // pass 2: the service with descriptors read from its buffer only (no inline descriptors in
-    // the command line), for an A/B on the same box
-    for (int svc = 0; svc < 3; ++svc) {
-        if (svc == 2) setenv("VPCSUM_SVC_INLINE", "0", 1);
+    // A/B passes on the same box: 2 = the service with descriptors read from its buffer only
+    // (no inline descriptors in the command line); 3 = frame loads clamped to the last chunk
+    // (re-loads) instead of predicated
+    static const char* names[4] = {"launch", "service", "service_no_inline", "service_clamped_loads"};
+    for (int svc = 0; svc < 4; ++svc) {
+        setenv("VPCSUM_SVC_INLINE", svc == 2 ? "0" : "1", 1);
+        setenv("VPCSUM_SVC_CLAMP", svc == 3 ? "1" : "0", 1);
         if (vpcsum_ctx_set_service(ctx, svc ? 200000 : 0)) {
             fprintf(stderr, "service: %s\n", vpcsum_last_error());
             return 1;
         }
-        printf("%s\"%s\": {", sep, svc == 2 ? "service_no_inline" : svc ? "service" : "launch");
+        printf("%s\"%s\": {", sep, names[svc]);
         sep = ", ";
         const char* sep2 = "";
         for (uint32_t b : {1u, 3u, 4u, 32u, 128u, 1024u, 8192u}) {
-            if (svc == 2 && b > 4) break;
+            if (svc >= 2 && b > 128) break;
             std::vector<double> us;
             for (int it = 0; it < iters + 20; ++it) {
                 uint64_t t = 0;

@@ -351,6 +351,8 @@ int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
     v.idle_ticks = (uint64_t)idle_us * 100u;   // s_memrealtime runs at 100 MHz
     const char* inl = getenv("VPCSUM_SVC_INLINE");
     v.inline_desc = !(inl && inl[0] == '0');
+    const char* clamp = getenv("VPCSUM_SVC_CLAMP");   // A/B tooling: 1 = clamped frame loads
+    v.mb->opts = (clamp && clamp[0] == '1') ? kSvcOptClampLoads : 0;
     v.on = true;
     return 0;
 }
@@ -643,9 +645,10 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
             return 0;
         }
         memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
-        // up to kZeroCopyWaveTeams packets: one wave per packet (variant 6, 64 lanes x 4 loads),
-        // so the batch is a few PCIe round trips deep instead of K2's per-unit iterations
-        const int variant = n <= kZeroCopyWaveTeams ? 6 : 0;
+        // up to kZeroCopyWaveTeams packets: one wave per packet (variant 12, 64 lanes x 4
+        // predicated loads), so the batch is a few PCIe round trips deep instead of K2's per-unit
+        // iterations, and no chunk is read twice over PCIe
+        const int variant = n <= kZeroCopyWaveTeams ? 12 : 0;
         VPC_CHECK(launch_csum(base, arena_len, s.dh_desc, n, s.dh_out, s.dh_status, nullptr,
                               mode & VPCSUM_MODE_VERIFY, (mode & VPCSUM_MODE_WRITE) ? base : nullptr, variant, 0,
                               s.stream),
@@ -742,7 +745,7 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
                                      nullptr, s.stream),
                   "parse launch");
         VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, s.dh_out, s.dh_status, nullptr, VPCSUM_MODE_VERIFY, nullptr,
-                              n <= kZeroCopyWaveTeams ? 6 : 0, 0, s.stream),
+                              n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
                   "verify launch");
     }
     VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");

@@ -27,7 +27,7 @@ struct alignas(64) SvcMailbox {
     uint64_t rsv0;
     vpcsum_desc_t idesc[kSvcInlineDesc];   // host: descriptors 0..2 of the batch, rsv = (uint8_t)seq
     alignas(64) uint64_t arena;   // line 1, device addresses, read when kSvcParams: arena, then
-    uint64_t arena_len, arena_w, desc, out, status, rsv[2];
+    uint64_t arena_len, arena_w, desc, out, status, opts, rsv;   // opts: kSvcOpt* (tooling)
     alignas(64) uint32_t done;   // device: last completed batch
     uint32_t pad_;
     uint64_t stamp[7];           // VPCSUM_SVC_STAMPS builds only: s_memrealtime per batch step
@@ -35,6 +35,7 @@ struct alignas(64) SvcMailbox {
 static_assert(sizeof(vpcsum_desc_t) * kSvcInlineDesc + 16 == 64, "SvcMailbox command line: one 64-B line");
 static_assert(offsetof(SvcMailbox, arena) == 64 && offsetof(SvcMailbox, done) == 128, "SvcMailbox line layout");
 constexpr uint64_t kSvcInline = 1ull << 60, kSvcStop = 1ull << 61, kSvcVerify = 1ull << 62, kSvcParams = 1ull << 63;
+constexpr uint64_t kSvcOptClampLoads = 1;   // A/B: the frame loads of a batch clamp instead of predicate
 constexpr uint32_t kSvcMaxPkts = (1u << 28) - 1;
 constexpr int kServiceGrid = 32;   // workgroups: 4 waves each, one packet per wave and round
 hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream);

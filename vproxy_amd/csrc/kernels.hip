@@ -138,7 +138,10 @@ struct PktPlan {
 
 // Body for workgroup `blk` of a grid of `gdim` workgroups (k_csum: the launch grid;
 // k_csum_service: the persistent service grid, once per batch).
-template <int TEAM, int U, bool VERIFY, bool NT>
+// PRED: chunks past the packet end are not loaded (exec-masked) instead of re-loading the last
+// chunk.  On device memory the clamped re-load is a cache hit and keeps the loads branch-free;
+// on uncached host memory (zero-copy frames) every such load is another PCIe read.
+template <int TEAM, int U, bool VERIFY, bool NT, bool PRED = false>
 __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -236,8 +239,13 @@ __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64
             for (int u = 0; u < U; ++u) {
                 // unconditional load (index clamped to the last chunk, a cache hit) keeps the
                 // U loads branch-free and in flight together; out-of-range chunks are skipped below
-                const int k = min((r0 + u) * TEAM + tl, pl.nch - 1);
-                v[u] = ld_stream<NT>(base + k);
+                if (PRED) {
+                    const int k = (r0 + u) * TEAM + tl;
+                    v[u] = k < pl.nch ? ld_stream<NT>(base + k) : make_uint4(0, 0, 0, 0);
+                } else {
+                    const int k = min((r0 + u) * TEAM + tl, pl.nch - 1);
+                    v[u] = ld_stream<NT>(base + k);
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -363,16 +371,16 @@ __device__ __forceinline__ uint32_t hw_bit(int b) { return (b >= 0 && b < 32) ? 
 // 2 halfword-select bits -> dword byte mask: bit0 -> 0x0000ffff, bit1 -> 0xffff0000
 __device__ __forceinline__ uint32_t hmask(uint32_t b) { return ((b & 1u) | ((b & 2u) << 15)) * 0xffffu; }
 
-template <int TEAM, int U, bool VERIFY, bool NT>
+template <int TEAM, int U, bool VERIFY, bool NT, bool PRED = false>
 __global__ __launch_bounds__(256) void k_csum(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                               const uint4* __restrict__ desc, uint32_t n,
                                               uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                               const uint8_t* __restrict__ flags_override,
                                               uint8_t* __restrict__ arena_w) {
-    k1_run<TEAM, U, VERIFY, NT>(arena, arena_len, desc, n, out, status, flags_override, arena_w, blockIdx.x, gridDim.x);
+    k1_run<TEAM, U, VERIFY, NT, PRED>(arena, arena_len, desc, n, out, status, flags_override, arena_w, blockIdx.x, gridDim.x);
 }
 
-template <int TEAM, int U>
+template <int TEAM, int U, bool PRED = false>
 static hipError_t launch_team(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                               uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                               uint8_t* arena_w, int grid, hipStream_t stream) {
@@ -382,7 +390,7 @@ static hipError_t launch_team(const uint8_t* arena, uint64_t arena_len, const vp
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum<TEAM, U, V, N>), dim3(g), dim3(256), 0, stream, arena, arena_len,                   \
+    hipLaunchKernelGGL((k_csum<TEAM, U, V, N, PRED>), dim3(g), dim3(256), 0, stream, arena, arena_len,                   \
                        (const uint4*)desc, n, out, status, flags_override, arena_w)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -815,7 +823,7 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                                                       uint64_t idle_ticks) {
     // batch parameters, read over PCIe by thread 0 when the host flags them as changed and kept
     // in LDS across batches: arena, arena_len, arena_w, desc, out, status
-    __shared__ uint64_t s_par[6];
+    __shared__ uint64_t s_par[7];
     __shared__ uint64_t s_cmd;
     __shared__ uint4 s_idesc[kSvcInlineDesc];   // workgroup 0: the inline descriptors of the batch
     __shared__ uint32_t s_inl;
@@ -897,6 +905,7 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                 s_par[3] = (uint64_t)q[1].z | ((uint64_t)q[1].w << 32);   // desc
                 s_par[4] = (uint64_t)q[2].x | ((uint64_t)q[2].y << 32);   // out
                 s_par[5] = (uint64_t)q[2].z | ((uint64_t)q[2].w << 32);   // status
+                s_par[6] = __builtin_nontemporal_load((const uint64_t*)&mb->opts);
             }
             s_cmd = got;
 #ifdef VPCSUM_SVC_STAMPS
@@ -913,6 +922,7 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         const uint4* desc = (blockIdx.x == 0 && s_inl) ? (const uint4*)s_idesc : (const uint4*)s_par[3];
         uint32_t* out = (uint32_t*)s_par[4];
         uint8_t* status = (uint8_t*)s_par[5];
+        const bool pred = (s_par[6] & kSvcOptClampLoads) == 0;
         __syncthreads();   // s_cmd / s_par are rewritten next round
         if (cmd == 0) return;
         have_par = true;
@@ -924,10 +934,17 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         // one wave per packet: a small flush is a few PCIe round trips deep (descriptor, frame
         // bytes, results) instead of K2's per-unit iterations, which a latency of ~3 us per
         // round trip would serialize
-        if (cmd & kSvcVerify)
-            k1_run<64, 4, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
-        else
-            k1_run<64, 4, false, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+        if (pred) {
+            if (cmd & kSvcVerify)
+                k1_run<64, 4, true, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+            else
+                k1_run<64, 4, false, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+        } else {
+            if (cmd & kSvcVerify)
+                k1_run<64, 4, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+            else
+                k1_run<64, 4, false, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+        }
         // the workgroup's stores are complete (barrier); thread 0 releases them system-wide and
         // counts the workgroup; the last participating workgroup publishes `done`
         __syncthreads();
@@ -1031,6 +1048,9 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 9: return VPC_T(8, 12);
         case 10: return VPC_T(16, 4);
         case 11: return VPC_T(8, 8);
+        // zero-copy frames in host memory: one wave per packet, predicated loads (k1_run PRED)
+        case 12: return launch_team<64, 4, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt,
+                                                 arena_w, grid > 0 ? grid : (int)default_grid(), stream);
         case 40: return launch_d<8, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 41: return launch_d<4, 12>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 43: return launch_d<16, 6>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
