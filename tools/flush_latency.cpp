@@ -49,40 +49,52 @@ int main(int argc, char** argv) {
         fprintf(stderr, "setup: %s\n", vpcsum_last_error());
         return 1;
     }
+    // A/B configurations on the same box: 2 = the service with descriptors read from its buffer
+    // only (no inline descriptors in the command line); 3 = frame loads clamped to the last chunk
+    // (re-loads) instead of predicated.  The configurations run interleaved in kRounds rounds of
+    // iters / kRounds flushes per size, so that drift on the box hits all of them alike.
+    static const char* names[4] = {"launch", "service", "service_no_inline", "service_clamped_loads"};
+    static const uint32_t sizes[7] = {1u, 3u, 4u, 32u, 128u, 1024u, 8192u};
+    constexpr int kRounds = 5;
+    std::vector<double> us[4][7];
+    for (int r = 0; r < kRounds; ++r) {
+        for (int svc = 0; svc < 4; ++svc) {
+            setenv("VPCSUM_SVC_INLINE", svc == 2 ? "0" : "1", 1);
+            setenv("VPCSUM_SVC_CLAMP", svc == 3 ? "1" : "0", 1);
+            if (vpcsum_ctx_set_service(ctx, svc ? 200000 : 0)) {
+                fprintf(stderr, "service: %s\n", vpcsum_last_error());
+                return 1;
+            }
+            for (int si = 0; si < 7; ++si) {
+                const uint32_t b = sizes[si];
+                if (svc >= 2 && b > 128) break;
+                for (int it = 0; it < iters / kRounds + 20; ++it) {
+                    uint64_t t = 0;
+                    const auto t0 = std::chrono::steady_clock::now();
+                    if (vpcsum_ctx_submit(ctx, arena.data(), arena.size(), desc.data(), b, out.data(), nullptr,
+                                          VPCSUM_MODE_WRITE, &t) ||
+                        vpcsum_ctx_wait(ctx, t)) {
+                        fprintf(stderr, "flush: %s\n", vpcsum_last_error());
+                        return 1;
+                    }
+                    const auto t1 = std::chrono::steady_clock::now();
+                    if (it >= 20) us[svc][si].push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+                }
+            }
+        }
+    }
     printf("{");
     const char* sep = "";
-    // A/B passes on the same box: 2 = the service with descriptors read from its buffer only
-    // (no inline descriptors in the command line); 3 = frame loads clamped to the last chunk
-    // (re-loads) instead of predicated
-    static const char* names[4] = {"launch", "service", "service_no_inline", "service_clamped_loads"};
     for (int svc = 0; svc < 4; ++svc) {
-        setenv("VPCSUM_SVC_INLINE", svc == 2 ? "0" : "1", 1);
-        setenv("VPCSUM_SVC_CLAMP", svc == 3 ? "1" : "0", 1);
-        if (vpcsum_ctx_set_service(ctx, svc ? 200000 : 0)) {
-            fprintf(stderr, "service: %s\n", vpcsum_last_error());
-            return 1;
-        }
         printf("%s\"%s\": {", sep, names[svc]);
         sep = ", ";
         const char* sep2 = "";
-        for (uint32_t b : {1u, 3u, 4u, 32u, 128u, 1024u, 8192u}) {
-            if (svc >= 2 && b > 128) break;
-            std::vector<double> us;
-            for (int it = 0; it < iters + 20; ++it) {
-                uint64_t t = 0;
-                const auto t0 = std::chrono::steady_clock::now();
-                if (vpcsum_ctx_submit(ctx, arena.data(), arena.size(), desc.data(), b, out.data(), nullptr,
-                                      VPCSUM_MODE_WRITE, &t) ||
-                    vpcsum_ctx_wait(ctx, t)) {
-                    fprintf(stderr, "flush: %s\n", vpcsum_last_error());
-                    return 1;
-                }
-                const auto t1 = std::chrono::steady_clock::now();
-                if (it >= 20) us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
-            }
-            std::sort(us.begin(), us.end());
-            printf("%s\"%u\": {\"median_us\": %.1f, \"p99_us\": %.1f}", sep2, b, us[us.size() / 2],
-                   us[(size_t)(us.size() * 0.99)]);
+        for (int si = 0; si < 7; ++si) {
+            std::vector<double>& v = us[svc][si];
+            if (v.empty()) continue;
+            std::sort(v.begin(), v.end());
+            printf("%s\"%u\": {\"median_us\": %.1f, \"p99_us\": %.1f}", sep2, sizes[si], v[v.size() / 2],
+                   v[(size_t)(v.size() * 0.99)]);
             sep2 = ", ";
         }
         printf("}");
