@@ -51,16 +51,18 @@ int main(int argc, char** argv) {
     }
     // A/B configurations on the same box: 2 = the service with descriptors read from its buffer
     // only (no inline descriptors in the command line); 3 = frame loads clamped to the last chunk
-    // (re-loads) instead of predicated.  The configurations run interleaved in kRounds rounds of
+    // (re-loads) instead of predicated; 4 = release semantics on the completion count and `done`.  The configurations run interleaved in kRounds rounds of
     // iters / kRounds flushes per size, so that drift on the box hits all of them alike.
-    static const char* names[4] = {"launch", "service", "service_no_inline", "service_clamped_loads"};
+    static const char* names[5] = {"launch", "service", "service_no_inline", "service_clamped_loads",
+                                  "service_release_done"};
     static const uint32_t sizes[7] = {1u, 3u, 4u, 32u, 128u, 1024u, 8192u};
     constexpr int kRounds = 5;
-    std::vector<double> us[4][7];
+    std::vector<double> us[5][7];
     for (int r = 0; r < kRounds; ++r) {
-        for (int svc = 0; svc < 4; ++svc) {
+        for (int svc = 0; svc < 5; ++svc) {
             setenv("VPCSUM_SVC_INLINE", svc == 2 ? "0" : "1", 1);
             setenv("VPCSUM_SVC_CLAMP", svc == 3 ? "1" : "0", 1);
+            setenv("VPCSUM_SVC_RELEASE_DONE", svc == 4 ? "1" : "0", 1);
             if (vpcsum_ctx_set_service(ctx, svc ? 200000 : 0)) {
                 fprintf(stderr, "service: %s\n", vpcsum_last_error());
                 return 1;
@@ -85,7 +87,7 @@ int main(int argc, char** argv) {
     }
     printf("{");
     const char* sep = "";
-    for (int svc = 0; svc < 4; ++svc) {
+    for (int svc = 0; svc < 5; ++svc) {
         printf("%s\"%s\": {", sep, names[svc]);
         sep = ", ";
         const char* sep2 = "";

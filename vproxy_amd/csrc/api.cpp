@@ -352,7 +352,8 @@ int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
     const char* inl = getenv("VPCSUM_SVC_INLINE");
     v.inline_desc = !(inl && inl[0] == '0');
     const char* clamp = getenv("VPCSUM_SVC_CLAMP");   // A/B tooling: 1 = clamped frame loads
-    v.mb->opts = (clamp && clamp[0] == '1') ? kSvcOptClampLoads : 0;
+    const char* reld = getenv("VPCSUM_SVC_RELEASE_DONE");   // A/B tooling: 1 = release on count / done
+    v.mb->opts = ((clamp && clamp[0] == '1') ? kSvcOptClampLoads : 0) | ((reld && reld[0] == '1') ? kSvcOptReleaseDone : 0);
     v.on = true;
     return 0;
 }

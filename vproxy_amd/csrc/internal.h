@@ -36,6 +36,7 @@ static_assert(sizeof(vpcsum_desc_t) * kSvcInlineDesc + 16 == 64, "SvcMailbox com
 static_assert(offsetof(SvcMailbox, arena) == 64 && offsetof(SvcMailbox, done) == 128, "SvcMailbox line layout");
 constexpr uint64_t kSvcInline = 1ull << 60, kSvcStop = 1ull << 61, kSvcVerify = 1ull << 62, kSvcParams = 1ull << 63;
 constexpr uint64_t kSvcOptClampLoads = 1;   // A/B: the frame loads of a batch clamp instead of predicate
+constexpr uint64_t kSvcOptReleaseDone = 2;  // A/B: release semantics on the completion count and `done`
 constexpr uint32_t kSvcMaxPkts = (1u << 28) - 1;
 constexpr int kServiceGrid = 32;   // workgroups: 4 waves each, one packet per wave and round
 hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream);

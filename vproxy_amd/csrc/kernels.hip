@@ -923,6 +923,7 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         uint32_t* out = (uint32_t*)s_par[4];
         uint8_t* status = (uint8_t*)s_par[5];
         const bool pred = (s_par[6] & kSvcOptClampLoads) == 0;
+        const bool rel_done = (s_par[6] & kSvcOptReleaseDone) != 0;
         __syncthreads();   // s_cmd / s_par are rewritten next round
         if (cmd == 0) return;
         have_par = true;
@@ -956,8 +957,16 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
 #ifdef VPCSUM_SVC_STAMPS
             if (blockIdx.x == 0) mb->stamp[3] = __builtin_amdgcn_s_memrealtime();
 #endif
-            // a batch of one workgroup (up to 4 frames) publishes without the device counter
-            const uint32_t d = nwg == 1 ? 0u : __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            // a batch of one workgroup (up to 4 frames) publishes without the device counter.
+            // The fence above has made this workgroup's results visible system-wide before the
+            // count, so the count needs no release of its own, and neither does the `done` store
+            // of a one-workgroup batch (one L2 write-back each).  With more workgroups `done`
+            // keeps its release: it must not overtake the counter reset, or the next batch's
+            // counts could land before it.  kSvcOptReleaseDone restores both (A/B tooling)
+            uint32_t d = 0;
+            if (nwg > 1)
+                d = rel_done ? __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
+                             : __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef VPCSUM_SVC_STAMPS
             if (blockIdx.x == 0) mb->stamp[4] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -968,7 +977,10 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 #endif
                 if (nwg > 1) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&mb->done, (uint32_t)cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (rel_done || nwg > 1)
+                    __hip_atomic_store(&mb->done, (uint32_t)cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                else
+                    __hip_atomic_store(&mb->done, (uint32_t)cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         }
