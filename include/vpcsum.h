@@ -82,23 +82,40 @@ typedef struct vpcsum_desc {
 #define VPCSUM_MODE_VERIFY   0x01u /* compute and compare with the stored fields (ingress)  */
 #define VPCSUM_MODE_WRITE    0x10u /* also write results big-endian into the arena in place */
 
-/* NAT rewrite entry for IPv4 packets (SwitchUtils.applyNat, SwitchUtils.java:522-542;
- * Ipv4Packet.setSrc/setDst :433-458, TcpPacket/UdpPacket.setSrcPort/setDstPort,
- * Ipv4Packet.setTtl :401-407 via IPInputRoute.java:79-91). All multi-byte values in
- * NETWORK byte order, exactly the bytes written into the packet. 16 bytes. */
-#define VPCSUM_NAT_SRC      0x01u
-#define VPCSUM_NAT_DST      0x02u
-#define VPCSUM_NAT_SPORT    0x04u
-#define VPCSUM_NAT_DPORT    0x08u
-#define VPCSUM_NAT_DEC_TTL  0x10u
+/* NAT / TTL rewrites (SwitchUtils.applyNat, core/.../vswitch/util/SwitchUtils.java:522-542): the
+ * setters Ipv4Packet.setSrc/setDst (vpacket/Ipv4Packet.java:433-458), Ipv6Packet.setSrc/setDst
+ * (Ipv6Packet.java:374-396), TcpPacket/UdpPacket.setSrcPort/setDstPort (TcpPacket.java:31-51,
+ * UdpPacket.java:188-209), Ipv4Packet.setTtl (:401-407; IPInputRoute.java:79-91 decrements) and
+ * Ipv6Packet.setHopLimit (:354-359), each followed by Java's recompute of the sums it dirtied.
+ * Address and port bytes in NETWORK byte order, exactly the bytes written into the packet. */
+#define VPCSUM_NAT_SRC      0x01u /* source address (IPv4 bytes 12..15 / IPv6 8..23)             */
+#define VPCSUM_NAT_DST      0x02u /* destination address (IPv4 16..19 / IPv6 24..39)              */
+#define VPCSUM_NAT_SPORT    0x04u /* TCP / UDP source port                                        */
+#define VPCSUM_NAT_DPORT    0x08u /* TCP / UDP destination port                                   */
+#define VPCSUM_NAT_DEC_TTL  0x10u /* IPv4 TTL / IPv6 hop limit minus 1 (after SET_TTL if both)    */
+#define VPCSUM_NAT_SET_TTL  0x20u /* IPv4 TTL / IPv6 hop limit := the entry's ttl value           */
+
+/* IPv4-only entry, 16 bytes (BASELINE config C5: 72 algorithmic bytes per packet).
+ * rsv[0] carries the VPCSUM_NAT_SET_TTL value; an IPv6 descriptor is rejected (S_BAD_DESC). */
 typedef struct vpcsum_nat4 {
     uint8_t  src[4];
     uint8_t  dst[4];
     uint8_t  sport[2];
     uint8_t  dport[2];
     uint8_t  mask;     /* VPCSUM_NAT_*  */
-    uint8_t  rsv[3];
+    uint8_t  rsv[3];   /* rsv[0]: TTL value for VPCSUM_NAT_SET_TTL, others 0 */
 } vpcsum_nat4_t;
+
+/* IPv4 and IPv6 entry, 48 bytes: an IPv4 packet uses src[0..3] / dst[0..3]. */
+typedef struct vpcsum_nat {
+    uint8_t  src[16];
+    uint8_t  dst[16];
+    uint8_t  sport[2];
+    uint8_t  dport[2];
+    uint8_t  mask;     /* VPCSUM_NAT_*                                  */
+    uint8_t  ttl;      /* TTL / hop limit value for VPCSUM_NAT_SET_TTL    */
+    uint8_t  rsv[10];  /* 0                                             */
+} vpcsum_nat_t;
 
 /* NAT modes. */
 #define VPCSUM_NAT_RFC1624     0x00u /* incremental update (RFC 1624 eqn. 3); header bytes only */
@@ -124,10 +141,15 @@ int vpcsum_compute_async(const uint8_t* d_arena, uint64_t arena_len,
                          uint32_t* d_out, uint8_t* d_status,
                          uint32_t mode, void* stream);
 
-/* NAT / TTL rewrite + checksum update, in place in the arena. */
+/* NAT / TTL rewrite + checksum update, in place in the arena; d_rw[i] rewrites packet i.
+ * d_status (n bytes): S_DONE, or S_BAD_DESC for a rejected descriptor (nothing written);
+ * required with VPCSUM_NAT_STRICT_JAVA. */
 int vpcsum_nat4_async(uint8_t* d_arena, uint64_t arena_len,
                       const vpcsum_desc_t* d_desc, const vpcsum_nat4_t* d_rw, uint32_t n,
                       uint8_t* d_status, uint32_t nat_mode, void* stream);
+int vpcsum_nat_async(uint8_t* d_arena, uint64_t arena_len,
+                     const vpcsum_desc_t* d_desc, const vpcsum_nat_t* d_rw, uint32_t n,
+                     uint8_t* d_status, uint32_t nat_mode, void* stream);
 
 /* Build descriptors on the GPU by parsing Ethernet frames (EthernetPacket.from,
  * Ipv4Packet.from, Ipv6Packet.from rules). frame i = [d_frame_off[i], +d_frame_len[i]).
@@ -205,6 +227,15 @@ int vpcsum_ctx_stats(vpcsum_ctx_t* ctx, uint64_t* service_batches, uint64_t* ser
 int vpcsum_ctx_verify_frames(vpcsum_ctx_t* ctx, const uint8_t* h_arena, uint64_t arena_len,
                              const uint64_t* h_frame_off, const uint32_t* h_frame_len, uint32_t n,
                              uint32_t* h_out, uint8_t* h_status, uint64_t* ticket);
+/* NAT / TTL rewrites of host frames (SwitchUtils.applyNat for a batch): h_rw[i] rewrites the
+ * packet of h_desc[i] in place in the caller's frames, with the checksums updated as Java's
+ * recompute leaves them (nat_mode as vpcsum_nat_async).  Frames in a registered arena are
+ * rewritten where they lie (zero-copy); others are staged to the device and their rewritten
+ * header bytes (L3 header through the L4 checksum field) copied back at vpcsum_ctx_wait.
+ * h_status (may be NULL): S_DONE / S_BAD_DESC per packet.  Frames of one batch must not overlap. */
+int vpcsum_ctx_nat_submit(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena_len,
+                          const vpcsum_desc_t* h_desc, const vpcsum_nat_t* h_rw, uint32_t n,
+                          uint8_t* h_status, uint32_t nat_mode, uint64_t* ticket);
 /* Pipelined host->device->host throughput helper: processes a host arena of n fixed-stride
  * frames in `chunks` double-buffered pieces over two streams (H2D || kernel || D2H). */
 int vpcsum_ctx_pipeline(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint32_t stride, uint32_t copy_bytes,
@@ -248,6 +279,10 @@ int Java_io_vproxy_vpcsum_VPCsum_submit(PNIEnv_vpcsum_long* env, int64_t ctx, vo
  *                     MemorySegment frameLen, int n, MemorySegment out, MemorySegment status) -> long ticket */
 int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                               void* frameOff, void* frameLen, int32_t n, void* out, void* status);
+/* VPCsum.natSubmit(long ctx, MemorySegment arena, long arenaLen, MemorySegment desc,
+ *                  MemorySegment rw, int n, MemorySegment status, int natMode) -> long ticket */
+int Java_io_vproxy_vpcsum_VPCsum_natSubmit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                           void* desc, void* rw, int32_t n, void* status, int32_t natMode);
 /* VPCsum.setService(long ctx, int idleUs) */
 int Java_io_vproxy_vpcsum_VPCsum_setService(PNIEnv_vpcsum_void* env, int64_t ctx, int32_t idleUs);
 /* VPCsum.waitFor(long ctx, long ticket) */

@@ -119,75 +119,238 @@ class L3Info:
     proto: int
 
 
+IP_PROTOCOL_ETHERIP, IPv6_NO_NEXT_HEADER = 97, 59            # Consts.java:29-30
+ETHER_TYPE_ARP = 0x0806
+TCP_OPTION_END, TCP_OPTION_NOP, TCP_OPTION_MSS, TCP_OPTION_WINDOW_SCALE = 0, 1, 2, 3
+
+
+def _u16(b, o):
+    return (b[o] << 8) | b[o + 1]
+
+
+def _arp_from(b: bytes) -> str | None:
+    """ArpPacket.from (ArpPacket.java:22-70): the length checks (extra bytes are cut, not refused)."""
+    if len(b) < 8:
+        return "input packet length too short for an arp packet"
+    hs, ps = b[4], b[5]
+    if len(b) < 8 + 2 * (hs + ps):
+        return "input packet length too short for an arp packet"
+    return None
+
+
+def _etherip(b: bytes) -> str | None:
+    """EtherIPPacket.initPartial / from (EtherIPPacket.java:32-71): >= 2 B, then the inner
+    Ethernet frame.  Its own errors propagate; an inner IP packet that fails to parse is kept as
+    PacketBytes (EthernetPacket.java:60-64), an inner ARP that fails does propagate."""
+    if len(b) < 2:
+        return "input packet length too short for an etherip packet"
+    inner = b[2:]
+    if len(inner) < 14:
+        return "input packet length too short for a ethernet packet"
+    typ, hl = _u16(inner, 12), 14
+    if typ == ETHER_TYPE_8021Q:
+        if len(inner) < 18:
+            return "input packet length too short for 802.1q ethernet packet"
+        typ, hl = _u16(inner, 16), 18
+    if typ == ETHER_TYPE_ARP:
+        return _arp_from(inner[hl:])
+    return None
+
+
+def _l4_init_partial(ver: int, proto: int, seg: bytes) -> str | None:
+    """Ipv4/Ipv6Packet.initUpperLayerPacket(.., raw) (Ipv4Packet.java:146-163, Ipv6Packet.java:
+    161-180) -> the L4 PartialPacket.initPartial: TcpPacket.java:187-199 (>= 20 B),
+    UdpPacket.java:17-27 (>= 8 B), IcmpPacket.java:22-26 (reads byte 0: a 0-byte ICMP message
+    throws in the reference -- refused here), EtherIPPacket.java:32-48."""
+    if proto == IP_PROTOCOL_TCP:
+        return "input packet length too short for a tcp packet" if len(seg) < 20 else None
+    if proto == IP_PROTOCOL_UDP:
+        return "input packet length too short for an udp packet" if len(seg) < 8 else None
+    if proto == IP_PROTOCOL_ICMP or (ver == 6 and proto == IP_PROTOCOL_ICMPv6):
+        return "icmp packet with no bytes (IndexOutOfBounds in the reference)" if len(seg) < 1 else None
+    if proto == IP_PROTOCOL_ETHERIP:
+        return _etherip(seg)
+    return None   # PacketBytes
+
+
+def _tcp_from(seg: bytes) -> str | None:
+    """TcpPacket.from (TcpPacket.java:223-287) incl. the option walk and TcpOption.from/check
+    (:602-640).  An option of length 0 re-reads itself forever in the reference and one of
+    length 1 throws (bytes.uint8(1) of a 1-byte view): both refused."""
+    if len(seg) < 20:
+        return "input packet length too short for a tcp packet"
+    data_off = ((seg[12] >> 4) & 0xF) * 4
+    if data_off > len(seg):
+        return "dataOffset too big"
+    off = 20
+    while data_off > 20 and off < data_off:
+        kind = seg[off]
+        if kind in (TCP_OPTION_END, TCP_OPTION_NOP):
+            off += 1
+            if kind == TCP_OPTION_END:
+                break
+            continue
+        if off + 1 >= data_off:
+            return "invalid tcp option, reaches dataOffset"
+        ln = seg[off + 1]
+        if off + ln > data_off:
+            return "invalid tcp option, length is too long"
+        if ln == 0:
+            return "tcp option of length 0 (the reference loops forever)"
+        if ln == 1:
+            return "tcp option of length 1 (IndexOutOfBounds in the reference)"
+        if kind == TCP_OPTION_WINDOW_SCALE and ln != 3:
+            return "invalid tcp option length for kind=window_scale"
+        if kind == TCP_OPTION_MSS and ln != 4:
+            return "invalid tcp option length for kind=mss"
+        off += ln
+    return None
+
+
+def _l4_from(ver: int, proto: int, seg: bytes) -> str | None:
+    """The L4 full parse (AbstractPacket.from): TcpPacket.from, UdpPacket.from (UdpPacket.java:
+    40-60: >= 8 B and the length field equal to the buffer), IcmpPacket.from (IcmpPacket.java:
+    33-45: >= 8 B), EtherIPPacket.from."""
+    if proto == IP_PROTOCOL_TCP:
+        return _tcp_from(seg)
+    if proto == IP_PROTOCOL_UDP:
+        if len(seg) < 8:
+            return "input packet length too short for an udp packet"
+        return "udp packet length not matching the input bytes length" if _u16(seg, 4) != len(seg) else None
+    if proto == IP_PROTOCOL_ICMP or (ver == 6 and proto == IP_PROTOCOL_ICMPv6):
+        return "input packet length too short for a icmp packet" if len(seg) < 8 else None
+    if proto == IP_PROTOCOL_ETHERIP:
+        return _etherip(seg)
+    return None
+
+
+def _ipv6_from(b: bytes, off: int) -> tuple[L3Info | None, str | None]:
+    """Ipv6Packet.from(raw, mustParse) (Ipv6Packet.java:69-159)."""
+    if len(b) < 40:
+        return None, "input packet length too short for an ipv6 packet"
+    if b[0] >> 4 != 6:
+        return None, f"invalid version for ipv6 packet: {b[0] >> 4}"
+    pl, nh = _u16(b, 4), b[6]
+    if pl == 0:
+        return None, "we do not support Jumbo Payload for now"
+    if 40 + pl > len(b):
+        return None, f"40+payloadLength({pl}) > input.length({len(b)})"
+    total = 40 + pl                     # setPktBufLen: L2 padding is cut
+    skip, proto = 0, nh
+    if nh in IPv6_needs_next_header:
+        # ExtHeader.from (Ipv6Packet.java ExtHeader): an ext header occupies 8 + hdrExtLen bytes
+        # (the reference's rule, not RFC 8200's (len+1)*8).  A chain of two or more re-parses the
+        # first one forever (xhBuf = xhBuf.sub(0, len)): refused.
+        xh = b[40:total]
+        if len(xh) < 8 or len(xh) < 8 + xh[1]:
+            return None, "input packet length too short for an ipv6 ext hdr packet"
+        if xh[0] in IPv6_needs_next_header:
+            return None, "multiple ipv6 ext headers (the reference loops forever)"
+        skip, proto = 8 + xh[1], xh[0]
+    seg = b[40 + skip:total]
+    if proto == IPv6_NO_NEXT_HEADER and len(seg) != 0:
+        return None, "NO_NEXT_HEADER with bytes for a next packet"
+    err = _l4_from(6, proto, seg)
+    if err:
+        return None, err
+    return L3Info(off, total, 40 + skip, 6, proto), None
+
+
+def _ipv4_from(b: bytes, off: int) -> tuple[L3Info | None, str | None]:
+    """Ipv4Packet.from (Ipv4Packet.java:73-145)."""
+    if len(b) < 20:
+        return None, "input packet length too short for an ip packet"
+    if b[0] >> 4 != 4:
+        return None, f"invalid version for ipv4 packet: {b[0] >> 4}"
+    ihl = b[0] & 0x0F
+    if len(b) < ihl * 4:
+        return None, f"input packet smaller than ihl({ihl}) specified"
+    if ihl < 5:
+        return None, f"input packet ihl({ihl}) < 5"
+    total = _u16(b, 2)
+    if total < ihl * 4:
+        return None, f"input ihl({ihl}) > totalLength({total})"
+    if total > len(b):
+        return None, f"totalLength({total}) > input.length({len(b)})"
+    err = _l4_from(4, b[9], b[ihl * 4:total])
+    if err:
+        return None, err
+    return L3Info(off, total, ihl * 4, 4, b[9]), None
+
+
 def parse_l3(buf: bytes, off: int, avail: int) -> tuple[L3Info | None, str | None]:
-    """Ipv4Packet.from (Ipv4Packet.java:73-145) / Ipv6Packet.from (Ipv6Packet.java:69-159)
-    reduced to the fields the checksum needs. Returns (info, err)."""
-    b = buf[off:off + avail]
+    """An IP packet without L2 (tun / FLAG_IP, PacketBuffer.init, PacketBuffer.java:156-174): the
+    version nibble picks Ipv4Packet.from / Ipv6Packet.from, full parse down to L4.  Returns
+    (info, err); err means vproxy refuses the packet (no checksum)."""
+    b = bytes(buf[off:off + avail])
     if len(b) < 1:
         return None, "empty"
     ver = b[0] >> 4
     if ver == 4:
-        if len(b) < 20:
-            return None, "input packet length too short for an ip packet"
-        ihl = b[0] & 0x0F
-        if len(b) < ihl * 4:
-            return None, f"input packet smaller than ihl({ihl}) specified"
-        if ihl < 5:
-            return None, f"input packet ihl({ihl}) < 5"
-        total = (b[2] << 8) | b[3]
-        if total < ihl * 4:
-            return None, f"input ihl({ihl}) > totalLength({total})"
-        if total > len(b):
-            return None, f"totalLength({total}) > input.length({len(b)})"
-        return L3Info(off, total, ihl * 4, 4, b[9]), None
+        return _ipv4_from(b, off)
     if ver == 6:
-        if len(b) < 40:
-            return None, "input packet length too short for an ipv6 packet"
-        pl = (b[4] << 8) | b[5]
-        nh = b[6]
-        if pl == 0:
-            return None, "we do not support Jumbo Payload for now"
-        if 40 + pl > len(b):
-            return None, f"40+payloadLength({pl}) > input.length({len(b)})"
-        total = 40 + pl
-        skip = 0
-        proto = nh
-        if nh in IPv6_needs_next_header:
-            # Ipv6Packet.java:121-139 / ExtHeader.from :199-211: an ext header occupies
-            # 8 + hdrExtLen bytes (the reference's rule, not RFC 8200's (len+1)*8).  A chain
-            # of more than one ext header re-parses the first one forever in the reference
-            # (xhBuf = xhBuf.sub(0, len)), so only single-ext-header packets are defined.
-            xh = b[40:total]
-            if len(xh) < 8:
-                return None, "input packet length too short for an ipv6 ext hdr packet"
-            nxt, hlen = xh[0], xh[1]
-            if len(xh) < 8 + hlen:
-                return None, "input packet length too short for an ipv6 ext hdr packet"
-            if nxt in IPv6_needs_next_header:
-                return None, "multiple ipv6 ext headers (reference loops forever)"
-            skip = 8 + hlen
-            proto = nxt
-        return L3Info(off, total, 40 + skip, 6, proto), None
-    return None, f"invalid version {ver}"
+        return _ipv6_from(b, off)
+    return None, f"receiving packet with unknown ip version: {ver}"
+
+
+def _ipv4_init_partial(b: bytes, off: int) -> tuple[L3Info | None, str | None]:
+    """Ipv4Packet.initPartial (Ipv4Packet.java:29-63): no version check (the EtherType chose
+    IPv4), the L4 part only through initPartial."""
+    if len(b) < 20:
+        return None, "input packet length too short for an ip packet"
+    ihl = b[0] & 0x0F
+    if len(b) < ihl * 4:
+        return None, f"input packet smaller than ihl({ihl}) specified"
+    if ihl < 5:
+        return None, f"input packet ihl({ihl}) < 5"
+    total = _u16(b, 2)
+    if total < ihl * 4:
+        return None, f"input ihl({ihl}) > totalLength({total})"
+    if total > len(b):
+        return None, f"totalLength({total}) > input.length({len(b)})"
+    err = _l4_init_partial(4, b[9], b[ihl * 4:total])
+    if err:
+        return None, err
+    return L3Info(off, total, ihl * 4, 4, b[9]), None
+
+
+def _ipv6_init_partial(b: bytes, off: int) -> tuple[L3Info | None, str | None]:
+    """Ipv6Packet.initPartial (Ipv6Packet.java:26-59): no version check, unless the next header
+    is an extension header -- then the full Ipv6Packet.from runs (L4 included)."""
+    if len(b) < 40:
+        return None, "input packet length too short for an ipv6 packet"
+    nh = b[6]
+    if nh in IPv6_needs_next_header:
+        return _ipv6_from(b, off)
+    pl = _u16(b, 4)
+    if pl == 0:
+        return None, "we do not support Jumbo Payload for now"
+    if 40 + pl > len(b):
+        return None, f"40+payloadLength({pl}) > input.length({len(b)})"
+    err = _l4_init_partial(6, nh, b[40:40 + pl])
+    if err:
+        return None, err
+    return L3Info(off, 40 + pl, 40, 6, nh), None
 
 
 def parse_ether(frame: bytes) -> tuple[L3Info | None, str | None]:
-    """EthernetPacket.from (EthernetPacket.java:25-94): 14 B header, 18 B with an 802.1Q tag."""
+    """An Ethernet frame as the vswitch receives it (tap / XDP: PacketBuffer.init ->
+    EthernetPacket.from(raw, allowPartial=true), EthernetPacket.java:25-94): 14 B header, 18 B
+    with an 802.1Q tag, then Ipv4Packet/Ipv6Packet.initPartial by EtherType.  An IP packet that
+    fails to parse becomes PacketBytes (:60-64): no checksum, reported here as an error."""
+    frame = bytes(frame)
     if len(frame) < 14:
         return None, "input packet length too short for a ethernet packet"
-    typ = (frame[12] << 8) | frame[13]
-    hl = 14
+    typ, hl = _u16(frame, 12), 14
     if typ == ETHER_TYPE_8021Q:
         if len(frame) < 18:
             return None, "input packet length too short for 802.1q ethernet packet"
-        typ = (frame[16] << 8) | frame[17]
-        hl = 18
-    if typ not in (ETHER_TYPE_IPv4, ETHER_TYPE_IPv6):
-        return None, "not ip"
-    info, err = parse_l3(frame, hl, len(frame) - hl)
-    if info is not None and ((typ == ETHER_TYPE_IPv4) != (info.ver == 4)):
-        return None, "version mismatch"
-    return info, err
+        typ, hl = _u16(frame, 16), 18
+    if typ == ETHER_TYPE_IPv4:
+        return _ipv4_init_partial(frame[hl:], hl)
+    if typ == ETHER_TYPE_IPv6:
+        return _ipv6_init_partial(frame[hl:], hl)
+    return None, "not ip"
 
 
 def desc_flags_for(info: L3Info, want_ip=True, want_l4=True) -> int:

@@ -887,3 +887,69 @@ def test_arena_beyond_4gib(V, orc):
         assert np.array_equal(got, a2[i * stride:(i + 1) * stride]), i
     del big
     torch.cuda.empty_cache()
+
+
+def test_parse_rules_on_gpu(V, orc):
+    """k_parse_ether and ctx_verify_frames against the oracle's parse on frames at every edge of
+    the reference's parse rules (tests/edgevec.py:parse_cases): TCP under 20 B, UDP under 8 B,
+    empty ICMP, the version nibble not read by initPartial, the full Ipv6Packet.from behind an
+    extension header (UDP length field, ICMP >= 8 B, TCP options), EtherIP, 802.1Q."""
+    import torch
+    import edgevec as E
+    cases = E.parse_cases()
+    offs, lens, arena = [], [], bytearray()
+    for i, (f, _, _) in enumerate(cases):
+        arena += bytes(i % 7)
+        offs.append(len(arena))
+        lens.append(len(f))
+        arena += f
+    arena = np.frombuffer(bytes(arena) + bytes(256), np.uint8).copy()
+    n = len(cases)
+    d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    V.parse_ether(dev(arena), dev(np.array(offs, np.uint64)), dev(np.array(lens, np.uint32)), n, d, st)
+    torch.cuda.synchronize()
+    got, stn = V.tensor_to_desc(d), st.cpu().numpy()
+    ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=n)
+    ctx.register(arena)
+    vout, vst = ctx.verify_frames(arena, np.array(offs), np.array(lens))
+    ctx.close()
+    for i, (f, ok, why) in enumerate(cases):
+        info, err = O.parse_ether(f)
+        assert (info is not None) == ok, why
+        if info is None:
+            assert stn[i] == O.S_BAD_DESC and vst[i] == O.S_BAD_DESC, why
+            continue
+        assert stn[i] == 0, why
+        g = got[i]
+        assert int(g["l3_off"]) == offs[i] + info.l3_off, why
+        assert (g["l3_len"], g["l4_off"], g["l3_ver"], g["l4_proto"]) == (info.l3_len, info.l4_off, info.ver, info.proto), why
+        assert g["flags"] == O.desc_flags_for(info), why
+        one = np.array([(offs[i] + info.l3_off, info.l3_len, info.l4_off, info.ver, info.proto,
+                         O.desc_flags_for(info), 0)], dtype=O.DESC_DTYPE)
+        o, s = orc.process(arena, one, O.MODE_VERIFY)
+        assert vst[i] == s[0] and vout[i] == o[0], why
+
+
+@pytest.mark.parametrize("service", [0, 20000])
+def test_unregister_with_batch_in_flight(V, orc, service):
+    """Unregistering an arena while a zero-copy batch (launched, or on the service grid) still
+    works on its frames finishes that batch first: the results are complete and the in-place
+    writes landed; the next batch from the (now pageable) arena is staged."""
+    n, stride = 300, 2048
+    a, d = orc.synth(n, stride, 14, O.SYNTH_C3, O.SEED, 606)
+    arena = np.concatenate([a, np.zeros(4096, np.uint8)])
+    want_arena = arena.copy()
+    want, _ = orc.process(want_arena, d, O.MODE_COMPUTE, write=True)
+    ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=n)
+    ctx.register(arena)
+    if service:
+        ctx.set_service(service)
+    out = np.zeros(n, np.uint32)
+    t = ctx.submit(arena, d, out, None, O.MODE_WRITE)
+    ctx.unregister(arena)
+    ctx.wait(t)
+    assert np.array_equal(out, want) and np.array_equal(arena, want_arena)
+    out2, _ = ctx.run(arena, d)
+    assert np.array_equal(out2, want)
+    ctx.close()

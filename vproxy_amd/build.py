@@ -10,8 +10,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libvpcsum.so")
-SOURCES = ["kernels.hip", "api.cpp"]
-HEADERS = ["internal.h", os.path.join("..", "..", "include", "vpcsum.h")]
+SOURCES = ["kernels.hip", "nat.hip", "api.cpp"]
+HEADERS = ["internal.h", "device_common.h", os.path.join("..", "..", "include", "vpcsum.h")]
 ARCH = os.environ.get("VPCSUM_ARCH", "gfx950")
 
 
@@ -36,7 +36,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     inc = ["-I", os.path.join(REPO, "include"), "-I", CSRC]
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"] + inc
-    for s in SOURCES:
+    procs = []
+    for s in SOURCES:   # the translation units compile in parallel
         src = os.path.join(CSRC, s)
         obj = os.path.join(CSRC, s + ".o")
         cmd = [hipcc()] + common + ["-c", src, "-o", obj]
@@ -44,8 +45,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
             cmd[1:1] = ["-x", "hip"]
         if verbose:
             print(" ".join(cmd))
-        subprocess.check_call(cmd)
+        procs.append((subprocess.Popen(cmd), cmd))
         objs.append(obj)
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:

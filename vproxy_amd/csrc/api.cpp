@@ -77,8 +77,12 @@ struct Slot {
     uint32_t* h_flen = nullptr;
     uint64_t* dh_foff = nullptr;
     uint32_t* dh_flen = nullptr;
+    vpcsum_nat_t* h_rw = nullptr;      // NAT rewrite tables: pinned staging (mapped) and device copy,
+    vpcsum_nat_t* dh_rw = nullptr;     // allocated with the context's first NAT batch
+    vpcsum_nat_t* d_rw = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    int kind = 0;                      // current batch: 0 checksums, 1 NAT rewrite
     bool zero_copy = false;            // current batch ran on the host frames in place
     uint32_t svc_seq = 0;              // != 0: the batch went to the low-latency service
     // the batch currently owned by this slot
@@ -193,26 +197,42 @@ int vpcsum_compute_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsu
     return 0;
 }
 
-int vpcsum_nat4_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const vpcsum_nat4_t* d_rw,
-                      uint32_t n, uint8_t* d_status, uint32_t nat_mode, void* stream) {
-    if (n == 0) return 0;
-    if (!d_arena || !d_desc || !d_rw) return fail("vpcsum_nat4_async: NULL arena, descriptors or rewrite table");
-    // tuning hints (not part of the stable ABI): bit 8 byte-access kernel, bits 12..14 packets
-    // per lane of the wide kernel
-    if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u | 0x7000u)) return fail("vpcsum_nat4_async: bad nat_mode 0x%x", nat_mode);
-    hipStream_t s = (hipStream_t)stream;
+// NAT on device memory: the rewrite kernel, then (strict Java) the full recompute of the sums it
+// dirtied, written in place -- Java's getRawPacket(0) after the setters.
+static int nat_run(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const void* d_rw, int fmt,
+                   uint32_t n, uint8_t* d_status, uint32_t nat_mode, hipStream_t s) {
     if (nat_mode & VPCSUM_NAT_STRICT_JAVA) {
-        if (!d_status) return fail("vpcsum_nat4_async: strict-java mode needs a status buffer");
         // pass 1: rewrite fields, record which sums went dirty (Java's checksumSkipped())
-        VPC_CHECK(launch_nat4(d_arena, arena_len, d_desc, d_rw, n, nullptr, d_status, nat_mode, s), "nat4 launch");
+        VPC_CHECK(launch_nat(d_arena, arena_len, d_desc, d_rw, fmt, n, nullptr, d_status, nat_mode, s), "nat launch");
         // pass 2: full recompute of the dirty sums, written in place (getRawPacket(0))
         VPC_CHECK(launch_csum(d_arena, arena_len, d_desc, n, nullptr, d_status, d_status, VPCSUM_MODE_WRITE, d_arena,
                               0, 0, s),
-                  "nat4 recompute launch");
+                  "nat recompute launch");
         return 0;
     }
-    VPC_CHECK(launch_nat4(d_arena, arena_len, d_desc, d_rw, n, d_status, nullptr, nat_mode, s), "nat4 launch");
+    VPC_CHECK(launch_nat(d_arena, arena_len, d_desc, d_rw, fmt, n, d_status, nullptr, nat_mode, s), "nat launch");
     return 0;
+}
+
+static int nat_async(const char* what, uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc,
+                     const void* d_rw, int fmt, uint32_t n, uint8_t* d_status, uint32_t nat_mode, void* stream) {
+    if (n == 0) return 0;
+    if (!d_arena || !d_desc || !d_rw) return fail("%s: NULL arena, descriptors or rewrite table", what);
+    // tuning hints (not part of the stable ABI): bit 8 byte-access kernel, bits 12..14 packets
+    // per lane of the wide kernel
+    if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u | 0x7000u)) return fail("%s: bad nat_mode 0x%x", what, nat_mode);
+    if ((nat_mode & VPCSUM_NAT_STRICT_JAVA) && !d_status) return fail("%s: strict-java mode needs a status buffer", what);
+    return nat_run(d_arena, arena_len, d_desc, d_rw, fmt, n, d_status, nat_mode, (hipStream_t)stream);
+}
+
+int vpcsum_nat4_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const vpcsum_nat4_t* d_rw,
+                      uint32_t n, uint8_t* d_status, uint32_t nat_mode, void* stream) {
+    return nat_async("vpcsum_nat4_async", d_arena, arena_len, d_desc, d_rw, 0, n, d_status, nat_mode, stream);
+}
+
+int vpcsum_nat_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const vpcsum_nat_t* d_rw,
+                     uint32_t n, uint8_t* d_status, uint32_t nat_mode, void* stream) {
+    return nat_async("vpcsum_nat_async", d_arena, arena_len, d_desc, d_rw, 1, n, d_status, nat_mode, stream);
 }
 
 int vpcsum_parse_ether_async(const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_frame_off,
@@ -297,6 +317,8 @@ static void slot_free(Slot& s) {
     if (s.h_arena) (void)hipHostFree(s.h_arena);
     if (s.h_foff) (void)hipHostFree(s.h_foff);
     if (s.h_flen) (void)hipHostFree(s.h_flen);
+    if (s.h_rw) (void)hipHostFree(s.h_rw);
+    if (s.d_rw) (void)hipFree(s.d_rw);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot();
@@ -433,8 +455,15 @@ int vpcsum_ctx_register_arena(vpcsum_ctx_t* c, void* h_arena, uint64_t len) {
 int vpcsum_ctx_unregister_arena(vpcsum_ctx_t* c, void* h_arena) {
     if (!c || !h_arena) return fail("vpcsum_ctx_unregister_arena: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
+    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
     for (size_t i = 0; i < c->registered.size(); ++i) {
         if (c->registered[i].host == (uint8_t*)h_arena) {
+            // a zero-copy batch (launched or on the service grid) may still read and write the
+            // frames in place: finish every such batch before the mapping goes away, and make the
+            // service re-read its parameters (they name this arena) with its next batch
+            for (auto& s : c->slots)
+                if (s.busy && s.zero_copy && slot_finish(c, s) != 0) return -1;
+            c->svc.par_valid = false;
             VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
             c->registered.erase(c->registered.begin() + i);
             return 0;
@@ -530,6 +559,24 @@ static int slot_finish(vpcsum_ctx* c, Slot& s) {
         if (svc_wait(c, s.svc_seq) != 0) return -1;
     } else {
         VPC_CHECK(hipEventSynchronize(s.done), "hipEventSynchronize");
+    }
+    if (s.kind == 1) {
+        // NAT: a staged batch's rewritten headers (L3 header through the L4 checksum field)
+        // go back into the caller's frames; zero-copy batches rewrote them in place
+        if (!s.zero_copy && s.user_arena) {
+            for (uint32_t i = 0; i < s.n; ++i) {
+                if (s.h_status[i] & VPCSUM_S_BAD_DESC) continue;
+                const vpcsum_desc_t& d = s.user_desc[i];
+                const int fld = d.l4_proto == 6 ? 16 : d.l4_proto == 17 ? 6 : (d.l4_proto == 1 || d.l4_proto == 58) ? 2 : -1;
+                uint32_t end = d.l3_ver == 4 ? 20 : 40;
+                if (fld >= 0 && d.l3_len >= d.l4_off + fld + 2) end = std::max<uint32_t>(end, d.l4_off + fld + 2u);
+                end = std::min<uint32_t>(end, d.l3_len);
+                memcpy(s.user_arena + d.l3_off, s.h_arena + s.h_desc[i].l3_off, end);
+            }
+        }
+        if (s.user_status) memcpy(s.user_status, s.h_status, s.n);
+        s.busy = false;
+        return 0;
     }
     const uint32_t* res_out = s.svc_seq ? c->svc.h_out : s.h_out;
     const uint8_t* res_status = s.svc_seq ? c->svc.h_status : s.h_status;
@@ -634,6 +681,7 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
             if (hipStreamQuery(v.stream) == hipSuccess && svc_launch(c, seq - 1) != 0) return -1;
             s.zero_copy = true;
             s.svc_seq = seq;
+            s.kind = 0;
             s.busy = true;
             s.ticket = t;
             s.n = n;
@@ -700,6 +748,7 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
         VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
     }
     VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+    s.kind = 0;
     s.busy = true;
     s.ticket = t;
     s.n = n;
@@ -752,6 +801,7 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
     VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
     s.zero_copy = true;
     s.svc_seq = 0;
+    s.kind = 0;
     s.busy = true;
     s.ticket = t;
     s.n = n;
@@ -759,6 +809,88 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
     s.user_arena = nullptr;
     s.user_desc = nullptr;
     s.user_out = h_out;
+    s.user_status = h_status;
+    *ticket = t;
+    return 0;
+}
+
+int vpcsum_ctx_nat_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                          const vpcsum_nat_t* h_rw, uint32_t n, uint8_t* h_status, uint32_t nat_mode, uint64_t* ticket) {
+    if (!c || !ticket) return fail("vpcsum_ctx_nat_submit: NULL context or ticket");
+    if (n > c->max_pkts) return fail("vpcsum_ctx_nat_submit: %u packets > capacity %u", n, c->max_pkts);
+    if (n && (!h_arena || !h_desc || !h_rw)) return fail("vpcsum_ctx_nat_submit: NULL arena, descriptors or rewrites");
+    if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u)) return fail("vpcsum_ctx_nat_submit: bad nat_mode 0x%x", nat_mode);
+    std::lock_guard<std::mutex> lk(c->mu);
+    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    const uint64_t t = c->next_ticket++;
+    Slot& s = c->slots[t & 1];
+    if (s.busy && slot_finish(c, s) != 0) return -1;
+    if (!s.h_rw) {
+        hipError_t e = hipSuccess;
+        const size_t bytes = (size_t)c->max_pkts * sizeof(vpcsum_nat_t);
+        if ((e = hipHostMalloc((void**)&s.h_rw, bytes, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&s.dh_rw, s.h_rw, 0)) != hipSuccess ||
+            (e = hipMalloc((void**)&s.d_rw, bytes)) != hipSuccess) {
+            if (s.h_rw) (void)hipHostFree(s.h_rw);
+            if (s.d_rw) (void)hipFree(s.d_rw);
+            s.h_rw = s.dh_rw = s.d_rw = nullptr;
+            return hipfail(e, "vpcsum_ctx_nat_submit allocation");
+        }
+    }
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const vpcsum_desc_t& d = h_desc[i];
+        if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) continue;   // the kernel flags it BAD
+        lo = std::min(lo, d.l3_off);
+        hi = std::max(hi, d.l3_off + d.l3_len);
+    }
+    if (lo == UINT64_MAX) { lo = 0; hi = 0; }
+    lo &= ~(uint64_t)15;
+    uint8_t* dev_arena = hi > lo ? mapped_dev(c, h_arena + lo, hi - lo) : nullptr;
+    memcpy(s.h_rw, h_rw, (size_t)n * sizeof(vpcsum_nat_t));
+    if (dev_arena) {
+        // the frames live in a registered (page-locked, mapped) arena: rewritten where they lie
+        memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
+        if (n && nat_run(dev_arena - lo, arena_len, s.dh_desc, s.dh_rw, 1, n, s.dh_status, nat_mode, s.stream) != 0)
+            return -1;
+        s.zero_copy = true;
+    } else {
+        // staged: each packet's 16-B blocks gathered into the pinned staging, rewritten on the
+        // device, and the whole gathered batch copied back (the headers return at wait)
+        uint64_t pos = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const vpcsum_desc_t& d = h_desc[i];
+            s.h_desc[i] = d;
+            if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) { s.h_desc[i].l3_off = UINT64_MAX; continue; }
+            const uint64_t a0 = d.l3_off & ~(uint64_t)15;
+            const uint64_t a1 = std::min<uint64_t>((d.l3_off + d.l3_len + 15) & ~(uint64_t)15, arena_len);
+            if (pos + (a1 - a0) > c->max_arena) return fail("vpcsum_ctx_nat_submit: batch exceeds the staging capacity");
+            memcpy(s.h_arena + pos, h_arena + a0, a1 - a0);
+            s.h_desc[i].l3_off = pos + (d.l3_off - a0);
+            pos += (a1 - a0 + 15) & ~(uint64_t)15;
+        }
+        if (n) {
+            VPC_CHECK(hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)n * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice, s.stream),
+                      "H2D descriptors");
+            VPC_CHECK(hipMemcpyAsync(s.d_rw, s.h_rw, (size_t)n * sizeof(vpcsum_nat_t), hipMemcpyHostToDevice, s.stream),
+                      "H2D rewrites");
+            if (pos) VPC_CHECK(hipMemcpyAsync(s.d_arena, s.h_arena, pos, hipMemcpyHostToDevice, s.stream), "H2D frames");
+            if (nat_run(s.d_arena, pos, s.d_desc, s.d_rw, 1, n, s.d_status, nat_mode, s.stream) != 0) return -1;
+            if (pos) VPC_CHECK(hipMemcpyAsync(s.h_arena, s.d_arena, pos, hipMemcpyDeviceToHost, s.stream), "D2H frames");
+            VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
+        }
+        s.zero_copy = false;
+    }
+    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+    s.kind = 1;
+    s.svc_seq = 0;
+    s.busy = true;
+    s.ticket = t;
+    s.n = n;
+    s.mode = nat_mode;
+    s.user_arena = h_arena;
+    s.user_desc = h_desc;
+    s.user_out = nullptr;
     s.user_status = h_status;
     *ticket = t;
     return 0;
@@ -875,6 +1007,21 @@ int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t c
     if (vpcsum_ctx_verify_frames((vpcsum_ctx_t*)(intptr_t)ctx, (const uint8_t*)arena, (uint64_t)arenaLen,
                                  (const uint64_t*)frameOff, (const uint32_t*)frameLen, (uint32_t)n, (uint32_t*)out,
                                  (uint8_t*)status, &t) != 0)
+        return pni_throw(env, "java.io.IOException");
+    env->return_ = (int64_t)t;
+    return 0;
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_natSubmit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                           void* desc, void* rw, int32_t n, void* status, int32_t natMode) {
+    if (n < 0 || arenaLen < 0) {
+        fail("natSubmit: negative size");
+        return pni_throw(env, "java.lang.IllegalArgumentException");
+    }
+    uint64_t t = 0;
+    if (vpcsum_ctx_nat_submit((vpcsum_ctx_t*)(intptr_t)ctx, (uint8_t*)arena, (uint64_t)arenaLen,
+                              (const vpcsum_desc_t*)desc, (const vpcsum_nat_t*)rw, (uint32_t)n, (uint8_t*)status,
+                              (uint32_t)natMode, &t) != 0)
         return pni_throw(env, "java.io.IOException");
     env->return_ = (int64_t)t;
     return 0;

@@ -41,8 +41,10 @@ constexpr uint32_t kSvcMaxPkts = (1u << 28) - 1;
 constexpr int kServiceGrid = 32;   // workgroups: 4 waves each, one packet per wave and round
 hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream);
 
-hipError_t launch_nat4(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const vpcsum_nat4_t* rw,
-                       uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream);
+// NAT / TTL rewrites (nat.hip).  fmt 0: rw is vpcsum_nat4_t[n], fmt 1: vpcsum_nat_t[n].  With
+// VPCSUM_NAT_STRICT_JAVA the kernel only rewrites and stores Java's dirty flags in flags_out.
+hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw, int fmt,
+                      uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream);
 
 hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const uint64_t* frame_off,
                               const uint32_t* frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* desc,

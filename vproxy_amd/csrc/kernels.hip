@@ -20,67 +20,13 @@
 #include <stdint.h>
 #include "vpcsum.h"
 #include "internal.h"
+#include "device_common.h"
 
 namespace vpcsum {
 
 // ------------------------------------------------------------------------------------------
 // small helpers
 // ------------------------------------------------------------------------------------------
-
-// Bytes of the dword at relative byte position d that fall inside [lo, hi).
-__device__ __forceinline__ uint32_t bmask(int d, int lo, int hi) {
-    int s = min(max(lo - d, 0), 4);
-    int e = min(max(hi - d, 0), 4);
-    uint32_t me = e >= 4 ? 0xffffffffu : ((1u << (e << 3)) - 1u);
-    uint32_t ms = s >= 4 ? 0xffffffffu : ((1u << (s << 3)) - 1u);
-    return me & ~ms;
-}
-
-// Bytes of the dword at relative position d that lie before `hi`.
-__device__ __forceinline__ uint32_t tailmask(int d, int hi) {
-    const int e = min(max(hi - d, 0), 4);
-    return e >= 4 ? 0xffffffffu : ((1u << (e << 3)) - 1u);
-}
-
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-
-// Packet bytes are read exactly once: non-temporal loads keep them from displacing the
-// descriptors and the next packets' lines in L2 / MALL (measured +10% on this pattern,
-// tools/bwlab.hip).
-// (address space 1 so hipcc emits global_load_dwordx4, not flat_load: flat loads count on
-// lgkmcnt too and force vmcnt(0)+lgkmcnt(0) waits that serialise the U loads in flight.)
-typedef __attribute__((address_space(1))) const u32x4_t gu32x4_t;
-template <bool NT>
-__device__ __forceinline__ uint4 ld_stream(const uint4* q) {
-    const u32x4_t v = NT ? __builtin_nontemporal_load((gu32x4_t*)q) : *(gu32x4_t*)q;
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-// End-around-carry fold of a 64-bit sum of LE words to 16 bits; 0 only for 0.
-__device__ __forceinline__ uint32_t fold64(uint64_t x) {
-    uint64_t t = (x & 0xffffffffull) + (x >> 32);
-    t = (t & 0xffff) + (t >> 16);
-    t = (t & 0xffff) + (t >> 16);
-    t = (t & 0xffff) + (t >> 16);
-    return (uint32_t)t;
-}
-__device__ __forceinline__ uint32_t fold32(uint32_t x) {
-    x = (x & 0xffff) + (x >> 16);
-    x = (x & 0xffff) + (x >> 16);
-    return x;
-}
-__device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xff) << 8) | (v >> 8); }
-// A sum taken over a byte range that starts at an even absolute address is byte-swapped
-// relative to the big-endian word grid of that range (RFC 1071 byte-order independence).
-__device__ __forceinline__ uint32_t orient(uint32_t v, int start) { return (start & 1) ? v : bswap16(v); }
-
-__device__ __forceinline__ int l4_field(int proto) {
-    return proto == 6 ? 16 : proto == 17 ? 6 : (proto == 1 || proto == 58) ? 2 : -1;
-}
-
-// Internal flag set by the NAT kernel on descriptors it rejected (strict-Java mode hands its
-// per-packet dirty flags to the checksum kernel through flags_override).
-constexpr int kFlagRejected = 0x80;
 
 // Default lanes per packet (large tier of K2) and 16-B loads in flight per lane.  The payload
 // loop costs the same per byte for any TEAM; 8 x 6 covers a 1500-B packet in two trips.
@@ -407,16 +353,8 @@ static hipError_t launch_team(const uint8_t* arena, uint64_t arena_len, const vp
 // the descriptor's range and the hardware returns zeros without touching memory.  So all U loads
 // of a lane are issued unconditionally (no branch, nothing for the compiler to sink), address
 // math is one 32-bit add per load, and the per-chunk classification is a single range test.
-// Needs a 16-B aligned arena < 4 GiB; launch_d falls back to k_csum otherwise.
+// Needs a 16-B aligned arena < 4 GiB (device_common.h); launch_d falls back to k_csum otherwise.
 // ------------------------------------------------------------------------------------------
-constexpr uint32_t kOutOfRange = 0xFFFFFF00u;
-constexpr uint64_t kMaxBufArena = 0xFFFF0000ull;
-// The range check zeroes any dword that reaches past num_records, so the descriptor covers the
-// arena rounded up to 16 B: the 16-B aligned block holding the last arena byte is readable
-// (it never crosses a page), and bytes past the arena end are masked by the packet bounds.
-__device__ __forceinline__ uint32_t buf_records(uint64_t arena_len) {
-    return (uint32_t)((arena_len + 15) & ~15ull);
-}
 
 // ------------------------------------------------------------------------------------------
 // K2: owner-lane plans, size-sorted teams.  A wave takes 64 consecutive packets per
@@ -971,6 +909,10 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
             if (blockIdx.x == 0) mb->stamp[4] = __builtin_amdgcn_s_memrealtime();
 #endif
             if (d + 1 == nwg) {
+                // the other workgroups' results were released at system scope by their own fences
+                // before their (relaxed) counts; this acquire orders the reset and `done` after
+                // them in the memory model as well (an L1 invalidate, no write-back)
+                if (nwg > 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #ifdef VPCSUM_SVC_STAMPS
                 mb->stamp[5] = __builtin_amdgcn_s_memrealtime();
                 mb->stamp[6] = s_ts;
@@ -1083,374 +1025,101 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
 }
 
 // ------------------------------------------------------------------------------------------
-// K5: NAT / TTL rewrite with RFC 1624 incremental update (one lane per packet).
-// Java writes the new bytes through the setters (Ipv4Packet.setSrc/setDst :433-458,
-// setTtl :401-407, TcpPacket/UdpPacket.setSrcPort/setDstPort) and recomputes the dirty sums
-// in full on the next getRawPacket(0) (SwitchUtils.applyNat, SwitchUtils.java:522-542).
-// RFC 1624 eqn. 3, HC' = ~(~HC + ~m + m'), is bit-identical to that full recompute whenever
-// the incoming checksum is correct; UDP with stored 0 is recomputed in full here.
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t ld16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
-__device__ __forceinline__ void st16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
-
-// Folded LE-absolute sum of bytes [lo, hi) (absolute addresses), one lane, aligned dwords.
-__device__ uint32_t lane_sum_range(const uint8_t* lo_p, const uint8_t* hi_p, const uint8_t* fld_p) {
-    const uintptr_t lo = (uintptr_t)lo_p, hi = (uintptr_t)hi_p, fa = (uintptr_t)fld_p;
-    const uintptr_t a = lo & ~(uintptr_t)3;
-    uint64_t acc = 0;
-    for (uintptr_t d = a; d < hi; d += 4) {
-        const uint32_t w = *(const __attribute__((address_space(1))) uint32_t*)d;
-        const int rd = (int)(d - a);
-        uint32_t m = bmask(rd, (int)(lo - a), (int)(hi - a));
-        if (fld_p) m &= ~bmask(rd, (int)(fa - a), (int)(fa - a) + 2);
-        acc += w & m;
-    }
-    return fold64(acc);
-}
-
-// One packet, byte accesses (IPv4 options, arenas the buffer path cannot address, or when the
-// wide kernel is disabled).
-__device__ void nat4_scalar(uint8_t* __restrict__ arena, uint64_t arena_len, const vpcsum_desc_t& d,
-                            const vpcsum_nat4_t& r, uint32_t p, uint8_t* __restrict__ status,
-                            uint8_t* __restrict__ flags_out, int strict) {
-    const uint64_t off = d.l3_off;
-    const int len = d.l3_len, l4o = d.l4_off;
-    if (off > arena_len || (uint64_t)len > arena_len - off || d.l3_ver != 4 || len < 20 || l4o < 20 ||
-        l4o > len || (l4o & 3)) {
-        if (status) status[p] = VPCSUM_S_BAD_DESC;
-        if (flags_out) flags_out[p] = kFlagRejected;
-        return;
-    }
-    uint8_t* l3 = arena + off;
-    const int proto = d.l4_proto;
-    const int fld = (proto == 6 || proto == 17) ? l4_field(proto) : -1;
-    const bool l4 = fld >= 0 && len - l4o >= fld + 2;
-    uint8_t* l4p = l3 + l4o;
-
-    // old / new 16-bit words; ip: header words, ps: pseudo words (+ ports for l4)
-    uint32_t ip_diff = 0;   // sum of ~m + m' over changed IP header words
-    uint32_t l4_diff = 0;   // sum of ~m + m' over changed pseudo/L4 words
-    bool ip_dirty = false, l4_dirty = false;
-    if (r.mask & VPCSUM_NAT_SRC) {
-        for (int i = 0; i < 2; ++i) {
-            const uint32_t m = ld16(l3 + 12 + 2 * i);
-            const uint32_t mn = ((uint32_t)r.src[2 * i] << 8) | r.src[2 * i + 1];
-            ip_diff += (~m & 0xffff) + mn;
-            l4_diff += (~m & 0xffff) + mn;
-            st16(l3 + 12 + 2 * i, mn);
-        }
-        ip_dirty = true; l4_dirty = true;
-    }
-    if (r.mask & VPCSUM_NAT_DST) {
-        for (int i = 0; i < 2; ++i) {
-            const uint32_t m = ld16(l3 + 16 + 2 * i);
-            const uint32_t mn = ((uint32_t)r.dst[2 * i] << 8) | r.dst[2 * i + 1];
-            ip_diff += (~m & 0xffff) + mn;
-            l4_diff += (~m & 0xffff) + mn;
-            st16(l3 + 16 + 2 * i, mn);
-        }
-        ip_dirty = true; l4_dirty = true;
-    }
-    if (r.mask & VPCSUM_NAT_DEC_TTL) {
-        const uint32_t m = ld16(l3 + 8);
-        const uint32_t mn = (((m >> 8) - 1) & 0xff) << 8 | (m & 0xff);
-        ip_diff += (~m & 0xffff) + mn;
-        st16(l3 + 8, mn);
-        ip_dirty = true;
-    }
-    if (l4) {
-        if (r.mask & VPCSUM_NAT_SPORT) {
-            const uint32_t m = ld16(l4p);
-            const uint32_t mn = ((uint32_t)r.sport[0] << 8) | r.sport[1];
-            l4_diff += (~m & 0xffff) + mn;
-            st16(l4p, mn);
-            l4_dirty = true;
-        }
-        if (r.mask & VPCSUM_NAT_DPORT) {
-            const uint32_t m = ld16(l4p + 2);
-            const uint32_t mn = ((uint32_t)r.dport[0] << 8) | r.dport[1];
-            l4_diff += (~m & 0xffff) + mn;
-            st16(l4p + 2, mn);
-            l4_dirty = true;
-        }
-    } else {
-        l4_dirty = false;
-    }
-    uint8_t fl = (ip_dirty ? VPCSUM_F_IP : 0) | (l4_dirty ? VPCSUM_F_L4 : 0);
-    if (strict) {
-        // Java semantics for any input: the csum kernel recomputes the dirty sums in full.
-        if (flags_out) flags_out[p] = fl;
-        return;
-    }
-    if (ip_dirty) {
-        const uint32_t hc = ld16(l3 + 10);
-        const uint32_t s = fold32((~hc & 0xffff) + fold32(ip_diff));
-        st16(l3 + 10, ~s & 0xffff);
-    }
-    if (l4_dirty) {
-        const uint32_t hc = ld16(l4p + fld);
-        uint32_t c;
-        if (proto == 17 && hc == 0) {
-            // "no checksum" UDP: Java recomputes the full sum (UdpPacket.java:136-149)
-            const uint32_t seg = orient(lane_sum_range(l4p, l3 + len, l4p + fld), (int)((uintptr_t)l4p & 1));
-            const uint32_t ps = orient(lane_sum_range(l3 + 12, l3 + 20, nullptr), (int)((uintptr_t)l3 & 1));
-            const uint32_t l4len = (uint32_t)(len - l4o);
-            c = 0xffff - fold32(seg + ps + 17u + l4len);
-        } else {
-            const uint32_t s = fold32((~hc & 0xffff) + fold32(l4_diff));
-            c = ~s & 0xffff;
-        }
-        if (proto == 17 && c == 0) c = 0xffff;
-        st16(l4p + fld, c);
-    }
-    if (status) status[p] = VPCSUM_S_DONE;
-}
-
-__global__ __launch_bounds__(256) void k_nat4(uint8_t* __restrict__ arena, uint64_t arena_len,
-                                             const vpcsum_desc_t* __restrict__ desc,
-                                             const vpcsum_nat4_t* __restrict__ rw, uint32_t n,
-                                             uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out,
-                                             int strict) {
-    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x)
-        nat4_scalar(arena, arena_len, desc[p], rw[p], p, status, flags_out, strict);
-}
-
-// Wide form (IPv4 without options, the C5 shape): the 64-B window holding bytes [8, 40) of the
-// packet is read with four 16-B buffer loads, staged in this lane's LDS slot, rewritten there
-// with byte-addressed LDS ops (the window's offset differs per packet), and the changed dwords
-// [8, 24) and the L4 checksum field are stored back as aligned dwords.  The scalar form needs
-// ~20 byte loads and ~20 byte stores per packet, each one wave instruction touching 64 lines.
-__device__ __forceinline__ uint32_t lds16(const uint8_t* w, int q) { return ((uint32_t)w[q] << 8) | w[q + 1]; }
-__device__ __forceinline__ void sts16(uint8_t* w, int q, uint32_t v) { w[q] = (uint8_t)(v >> 8); w[q + 1] = (uint8_t)v; }
-
-// One packet of the wide form, after its window arrived: stage in this lane's LDS slot `w`,
-// rewrite, store back.  `wide` false: the packet takes the byte-access path instead.
-template <bool STRICT>
-__device__ __forceinline__ void nat4w_apply(uint8_t* __restrict__ arena, uint64_t arena_len,
-                                            const vpcsum_desc_t* __restrict__ desc,
-                                            const vpcsum_nat4_t* __restrict__ rw, uint32_t p, const uint4 dv,
-                                            const uint4 rv, bool wide, const uint4* v, uint8_t* w,
-                                            uint2 (*slot)[9], uint8_t* __restrict__ status,
-                                            uint8_t* __restrict__ flags_out) {
-    if (!wide) {
-        nat4_scalar(arena, arena_len, desc[p], rw[p], p, status, flags_out, STRICT ? 1 : 0);
-        return;
-    }
-    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-    const int len = dv.z & 0xffff;
-    const int proto = (dv.w >> 8) & 0xff;
-    const int mask = rv.w & 0xff;
-    const int fld = (proto == 6 || proto == 17) ? l4_field(proto) : -1;
-    const bool l4 = fld >= 0 && len - 20 >= fld + 2;
-    const int r0 = (int)(off & 15);
-    const uint32_t boff = (uint32_t)(off - (uint64_t)r0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        (*slot)[2 * k] = make_uint2(v[k].x, v[k].y);
-        (*slot)[2 * k + 1] = make_uint2(v[k].z, v[k].w);
-    }
-    const int b = r0;   // packet byte 0 inside the window
-    uint32_t ip_diff = 0, l4_diff = 0;
-    bool ip_dirty = false, l4_dirty = false;
-    if (mask & VPCSUM_NAT_SRC) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const uint32_t m = lds16(w, b + 12 + 2 * i);
-            const uint32_t mn = (((rv.x >> (16 * i)) & 0xff) << 8) | ((rv.x >> (16 * i + 8)) & 0xff);
-            ip_diff += (~m & 0xffff) + mn;
-            l4_diff += (~m & 0xffff) + mn;
-            sts16(w, b + 12 + 2 * i, mn);
-        }
-        ip_dirty = true; l4_dirty = true;
-    }
-    if (mask & VPCSUM_NAT_DST) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const uint32_t m = lds16(w, b + 16 + 2 * i);
-            const uint32_t mn = (((rv.y >> (16 * i)) & 0xff) << 8) | ((rv.y >> (16 * i + 8)) & 0xff);
-            ip_diff += (~m & 0xffff) + mn;
-            l4_diff += (~m & 0xffff) + mn;
-            sts16(w, b + 16 + 2 * i, mn);
-        }
-        ip_dirty = true; l4_dirty = true;
-    }
-    if (mask & VPCSUM_NAT_DEC_TTL) {
-        const uint32_t m = lds16(w, b + 8);
-        const uint32_t mn = (((m >> 8) - 1) & 0xff) << 8 | (m & 0xff);
-        ip_diff += (~m & 0xffff) + mn;
-        sts16(w, b + 8, mn);
-        ip_dirty = true;
-    }
-    if (l4) {
-        if (mask & VPCSUM_NAT_SPORT) {
-            const uint32_t m = lds16(w, b + 20);
-            const uint32_t mn = ((rv.z & 0xff) << 8) | ((rv.z >> 8) & 0xff);
-            l4_diff += (~m & 0xffff) + mn;
-            sts16(w, b + 20, mn);
-            l4_dirty = true;
-        }
-        if (mask & VPCSUM_NAT_DPORT) {
-            const uint32_t m = lds16(w, b + 22);
-            const uint32_t mn = (((rv.z >> 16) & 0xff) << 8) | ((rv.z >> 24) & 0xff);
-            l4_diff += (~m & 0xffff) + mn;
-            sts16(w, b + 22, mn);
-            l4_dirty = true;
-        }
-    } else {
-        l4_dirty = false;
-    }
-    bool udp_zero = false;
-    if (!STRICT) {
-        if (ip_dirty) {
-            const uint32_t hc = lds16(w, b + 10);
-            sts16(w, b + 10, ~fold32((~hc & 0xffff) + fold32(ip_diff)) & 0xffff);
-        }
-        if (l4_dirty) {
-            const uint32_t hc = lds16(w, b + 20 + fld);
-            if (proto == 17 && hc == 0) {
-                udp_zero = true;   // recomputed in full below, after the new header is stored
-            } else {
-                uint32_t c = ~fold32((~hc & 0xffff) + fold32(l4_diff)) & 0xffff;
-                if (proto == 17 && c == 0) c = 0xffff;
-                sts16(w, b + 20 + fld, c);
-            }
-        }
-    }
-    // store back: dwords covering [8, 24) when anything in the IP header or ports changed,
-    // and the dword(s) of the L4 checksum field; a dword reaching past the packet end is
-    // stored bytewise (the neighbouring bytes may belong to another packet).
-    const uint32_t* wd = (const uint32_t*)w;
-    const int lim = r0 + len;
-    auto put = [&](int j) {
-        if (4 * j + 4 <= lim) {
-            *(__attribute__((address_space(1))) uint32_t*)(arena + boff + 4 * j) = wd[j];
-        } else {
-            for (int q = 4 * j; q < lim; ++q) arena[boff + q] = w[q];
-        }
-    };
-    if (ip_dirty || l4_dirty) {
-        const int j1 = (r0 + 23) >> 2;
-        for (int j = (r0 + 8) >> 2; j <= j1; ++j) put(j);
-        if (!STRICT && l4_dirty && !udp_zero) {
-            const int f = r0 + 20 + fld;
-            for (int j = max(f >> 2, j1 + 1); j <= (f + 1) >> 2; ++j) put(j);
-        }
-    }
-    const uint8_t fl = (ip_dirty ? VPCSUM_F_IP : 0) | (l4_dirty ? VPCSUM_F_L4 : 0);
-    if (STRICT) {
-        if (flags_out) flags_out[p] = fl;
-        return;
-    }
-    if (udp_zero) {
-        // "no checksum" UDP: Java recomputes the full sum (UdpPacket.java:136-149)
-        uint8_t* l3 = arena + off;
-        uint8_t* l4p = l3 + 20;
-        const uint32_t seg = orient(lane_sum_range(l4p, l3 + len, l4p + fld), (int)((uintptr_t)l4p & 1));
-        const uint32_t ps = orient(lane_sum_range(l3 + 12, l3 + 20, nullptr), (int)((uintptr_t)l3 & 1));
-        uint32_t c = 0xffff - fold32(seg + ps + 17u + (uint32_t)(len - 20));
-        if (c == 0) c = 0xffff;
-        st16(l4p + fld, c);
-    }
-    if (status) status[p] = VPCSUM_S_DONE;
-}
-
-// W packets per lane and iteration (p, p + T, ..., T = lanes of the grid): all their
-// descriptor / rewrite loads, then all their window loads are issued before the first packet
-// is rewritten, so a lane keeps W header windows in flight instead of one (the kernel is
-// latency-bound: ~4 dependent memory steps per packet).  The LDS slot is reused per packet.
-template <bool STRICT, int W>
-__global__ __launch_bounds__(256) void k_nat4w(uint8_t* __restrict__ arena, uint64_t arena_len,
-                                              const vpcsum_desc_t* __restrict__ desc,
-                                              const vpcsum_nat4_t* __restrict__ rw, uint32_t n,
-                                              uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out) {
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    // 72-B slot per lane (64-B window + 8): an 18-dword stride keeps byte ops <= 2-way on banks
-    __shared__ uint2 s_win[256][9];
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
-    uint8_t* w = (uint8_t*)&s_win[threadIdx.x][0];
-    const uint32_t T = gridDim.x * blockDim.x;
-    for (uint32_t p0 = blockIdx.x * blockDim.x + threadIdx.x; p0 < n; p0 += W * T) {
-        uint4 dv[W], rv[W];
-        bool wide[W];
-        uint4 v[W][4];
-#pragma unroll
-        for (int i = 0; i < W; ++i) {
-            const uint32_t p = p0 + i * T;
-            dv[i] = p < n ? ((const uint4*)desc)[p] : make_uint4(0, 0, 0, 0);
-            rv[i] = p < n ? ((const uint4*)rw)[p] : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < W; ++i) {
-            const uint32_t p = p0 + i * T;
-            const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
-            const int len = dv[i].z & 0xffff, l4o = dv[i].z >> 16;
-            const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
-            wide[i] = p < n && !(l4o != 20 || ver != 4 || off > arena_len || (uint64_t)len > arena_len - off || len < 20);
-            const int fld = (proto == 6 || proto == 17) ? l4_field(proto) : -1;
-            const bool l4 = fld >= 0 && len - 20 >= fld + 2;
-            const int r0 = (int)(off & 15);
-            const uint32_t boff = (uint32_t)(off - (uint64_t)r0);
-            const int wend = wide[i] ? r0 + (l4 ? 22 + fld : 24) : 0;   // window bytes needed
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (k << 4) < wend ? boff + (k << 4) : kOutOfRange, 0, 0);
-                v[i][k] = make_uint4(x.x, x.y, x.z, x.w);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < W; ++i) {
-            const uint32_t p = p0 + i * T;
-            if (p < n)
-                nat4w_apply<STRICT>(arena, arena_len, desc, rw, p, dv[i], rv[i], wide[i], v[i], w,
-                                    &s_win[threadIdx.x], status, flags_out);
-        }
-    }
-}
-
-constexpr int kNatWideLog2 = 1;   // packets per lane and iteration of k_nat4w: 2
-
-hipError_t launch_nat4(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const vpcsum_nat4_t* rw,
-                       uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const bool strict = (nat_mode & VPCSUM_NAT_STRICT_JAVA) != 0;
-    // nat_mode bits 12..14 (internal tuning): log2 packets per lane and iteration of the wide
-    // kernel + 1 (0 = default)
-    const int wsel = (int)((nat_mode >> 12) & 7u);
-    const int wl2 = wsel ? (wsel - 1 > 2 ? 2 : wsel - 1) : kNatWideLog2;
-    // one iteration of W packets per lane covers the batch when the chip holds the grid
-    uint32_t g = (n + (256u << wl2) - 1) / (256u << wl2);
-    uint32_t cap = (uint32_t)num_cus(dev) * 8;
-    if (g > cap) g = cap;
-    // nat_mode bit 8 (internal tuning): force the byte-access kernel
-    const bool wide = !(nat_mode & 0x100u) && arena_len <= kMaxBufArena && !((uintptr_t)arena & 15);
-    if (wide) {
-#define VPC_NAT(S, W) hipLaunchKernelGGL((k_nat4w<S, W>), dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out)
-        if (strict) {
-            if (wl2 == 0) VPC_NAT(true, 1); else if (wl2 == 1) VPC_NAT(true, 2); else VPC_NAT(true, 4);
-        } else {
-            if (wl2 == 0) VPC_NAT(false, 1); else if (wl2 == 1) VPC_NAT(false, 2); else VPC_NAT(false, 4);
-        }
-#undef VPC_NAT
-    } else {
-        hipLaunchKernelGGL(k_nat4, dim3(g), dim3(256), 0, stream, arena, arena_len, desc, rw, n, status, flags_out,
-                           strict ? 1 : 0);
-    }
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------
-// Parse kernel (one lane per frame): EthernetPacket.from (EthernetPacket.java:25-94) ->
-// Ipv4Packet.from (Ipv4Packet.java:73-145) / Ipv6Packet.from (Ipv6Packet.java:69-159),
-// reduced to what the checksum needs.  IPv6 extension headers follow the reference's
-// ExtHeader.from (Ipv6Packet.java ExtHeader: 8 + hdrExtLen bytes); a chain of two or more
-// makes the reference loop forever, so such frames are rejected.
+// Parse kernel (one lane per frame): an Ethernet frame as the vswitch receives it (tap / XDP:
+// PacketBuffer.init -> EthernetPacket.from(raw, allowPartial=true), EthernetPacket.java:25-94),
+// reduced to what the checksum needs.  The EtherType picks Ipv4Packet.initPartial
+// (Ipv4Packet.java:29-63, no version check) or Ipv6Packet.initPartial (Ipv6Packet.java:26-59, no
+// version check unless an extension header forces the full Ipv6Packet.from, :69-159).  The L4
+// part follows initPartial (TCP >= 20 B, UDP >= 8 B, ICMP >= 1 B) or, behind an extension header,
+// the full from() (TCP options, the UDP length field, ICMP >= 8 B).  A frame whose IP packet the
+// reference refuses (it becomes PacketBytes, EthernetPacket.java:60-64) gets S_BAD_DESC: no
+// checksum applies to it.  Extension headers follow the reference's ExtHeader.from (8 + hdrExtLen
+// bytes); a chain of two or more, and a TCP option of length 0, make the reference loop forever,
+// and a TCP option of length 1 or an empty ICMP message make it throw: such frames are refused.
+// Restated in Python by oracle/oracle.py:parse_ether (the tests compare the two frame by frame).
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool v6_needs_next(int h) {
     return h == 0 || h == 60 || h == 43 || h == 44 || h == 51 || h == 50 || h == 135 || h == 139 || h == 140 ||
            h == 253 || h == 254;
+}
+
+// EtherIPPacket.initPartial / from (EtherIPPacket.java:32-71): >= 2 B, the inner Ethernet header,
+// and an inner ARP that parses (ArpPacket.java:22-70); inner IP failures do not propagate.
+__device__ bool pe_etherip(const uint8_t* s, uint32_t len) {
+    if (len < 2) return false;
+    const uint8_t* f = s + 2;
+    const uint32_t L = len - 2;
+    if (L < 14) return false;
+    uint32_t typ = ld16(f + 12), hl = 14;
+    if (typ == 0x8100) {
+        if (L < 18) return false;
+        typ = ld16(f + 16);
+        hl = 18;
+    }
+    if (typ == 0x0806) {
+        const uint32_t a = L - hl;
+        if (a < 8) return false;
+        const uint32_t hs = f[hl + 4], ps = f[hl + 5];
+        if (a < 8 + 2 * (hs + ps)) return false;
+    }
+    return true;
+}
+
+// TcpPacket.from (TcpPacket.java:223-287) with the option walk and TcpOption.check (:602-640).
+__device__ bool pe_tcp_from(const uint8_t* s, uint32_t len) {
+    if (len < 20) return false;
+    const uint32_t doff = ((s[12] >> 4) & 15u) * 4u;
+    if (doff > len) return false;
+    if (doff > 20) {
+        uint32_t off = 20;
+        while (off < doff) {   // at most 40 option bytes
+            const uint32_t kind = s[off];
+            if (kind == 0 || kind == 1) {
+                off += 1;
+                if (kind == 0) break;
+                continue;
+            }
+            if (off + 1 >= doff) return false;
+            const uint32_t ln = s[off + 1];
+            if (off + ln > doff || ln < 2) return false;
+            if ((kind == 3 && ln != 3) || (kind == 2 && ln != 4)) return false;
+            off += ln;
+        }
+    }
+    return true;
+}
+
+// The upper-layer packet of an IP packet: initPartial (partial = true; TcpPacket.java:187-199,
+// UdpPacket.java:17-27, IcmpPacket.java:22-26) or the full from() (UdpPacket.java:40-60,
+// IcmpPacket.java:33-45).  ICMPv6 exists only inside IPv6 (Ipv4Packet.java:146-163 maps 58 to
+// PacketBytes); anything without a parser is PacketBytes and always accepted.
+__device__ bool pe_l4(bool partial, int ver, int proto, const uint8_t* s, uint32_t len) {
+    if (proto == 6) return partial ? len >= 20 : pe_tcp_from(s, len);
+    if (proto == 17) return partial ? len >= 8 : (len >= 8 && ld16(s + 4) == len);
+    if (proto == 1 || (ver == 6 && proto == 58)) return partial ? len >= 1 : len >= 8;
+    if (proto == 97) return pe_etherip(s, len);
+    return true;
+}
+
+// Ipv6Packet.from (Ipv6Packet.java:69-159) over avail bytes at b.
+__device__ bool pe_ipv6_from(const uint8_t* b, uint32_t avail, uint32_t& total, int& l4o, int& proto) {
+    if (avail < 40 || (b[0] >> 4) != 6) return false;
+    const uint32_t pl = ld16(b + 4);
+    const int nh = b[6];
+    if (pl == 0 || 40 + pl > avail) return false;
+    total = 40 + pl;
+    proto = nh;
+    l4o = 40;
+    if (v6_needs_next(nh)) {
+        if (pl < 8) return false;
+        const int nxt = b[40], hlen = b[41];
+        if (pl < (uint32_t)(8 + hlen) || v6_needs_next(nxt)) return false;
+        proto = nxt;
+        l4o = 40 + 8 + hlen;
+    }
+    const uint32_t seg = total - (uint32_t)l4o;
+    if (proto == 59 && seg != 0) return false;   // IPv6_NEXT_HEADER_NO_NEXT_HEADER with bytes
+    return pe_l4(false, 6, proto, b + l4o, seg);
 }
 
 __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__ arena, uint64_t arena_len,
@@ -1459,53 +1128,50 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
                                                     vpcsum_desc_t* __restrict__ desc, uint8_t* __restrict__ status) {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const uint64_t o = foff[p];
-        uint32_t L = flen[p];
+        const uint32_t L = flen[p];
         vpcsum_desc_t d;
         d.l3_off = 0; d.l3_len = 0; d.l4_off = 0; d.l3_ver = 0; d.l4_proto = 0; d.flags = 0; d.rsv = 0;
         uint8_t st = VPCSUM_S_BAD_DESC;
         bool ok = o <= arena_len && (uint64_t)L <= arena_len - o && L >= 14;
         const uint8_t* f = arena + o;
-        int hl = 14, typ = 0;
+        uint32_t hl = 14, typ = 0;
         if (ok) {
             typ = ld16(f + 12);
             if (typ == 0x8100) {
                 if (L < 18) ok = false;
                 else { typ = ld16(f + 16); hl = 18; }
             }
-            ok = ok && (typ == 0x0800 || typ == 0x86DD);
         }
         if (ok) {
             const uint8_t* b = f + hl;
             const uint32_t avail = L - hl;
-            const int ver = avail >= 1 ? (b[0] >> 4) : 0;
-            if (typ == 0x0800 && ver == 4 && avail >= 20) {
-                const int ihl = b[0] & 15;
+            if (typ == 0x0800 && avail >= 20) {
+                // Ipv4Packet.initPartial: the EtherType decided IPv4, the version nibble is not read
+                const uint32_t ihl = b[0] & 15u;
                 const uint32_t total = ld16(b + 2);
-                if (avail >= (uint32_t)ihl * 4 && ihl >= 5 && total >= (uint32_t)ihl * 4 && total <= avail) {
+                if (avail >= ihl * 4 && ihl >= 5 && total >= ihl * 4 && total <= avail &&
+                    pe_l4(true, 4, b[9], b + ihl * 4, total - ihl * 4)) {
                     d.l3_off = o + hl; d.l3_len = (uint16_t)total; d.l4_off = (uint16_t)(ihl * 4);
                     d.l3_ver = 4; d.l4_proto = b[9];
                     st = 0;
                 }
-            } else if (typ == 0x86DD && ver == 6 && avail >= 40) {
-                const uint32_t pl = ld16(b + 4);
-                const int nh = b[6];
-                if (pl != 0 && 40 + pl <= avail) {
-                    const uint32_t total = 40 + pl;
-                    int proto = nh, l4o = 40;
-                    bool good = true;
-                    if (v6_needs_next(nh)) {
-                        if (total - 40 < 8) good = false;
-                        else {
-                            const int nxt = b[40], hlen = b[41];
-                            if (total - 40 < (uint32_t)(8 + hlen) || v6_needs_next(nxt)) good = false;
-                            else { proto = nxt; l4o = 40 + 8 + hlen; }
-                        }
-                    }
-                    if (good && total <= 0xffff) {
-                        d.l3_off = o + hl; d.l3_len = (uint16_t)total; d.l4_off = (uint16_t)l4o;
-                        d.l3_ver = 6; d.l4_proto = (uint8_t)proto;
-                        st = 0;
-                    }
+            } else if (typ == 0x86DD && avail >= 40) {
+                uint32_t total = 0;
+                int l4o = 40, proto = b[6];
+                bool good;
+                if (v6_needs_next(b[6])) {
+                    good = pe_ipv6_from(b, avail, total, l4o, proto);   // initPartial defers to from()
+                } else {
+                    const uint32_t pl = ld16(b + 4);
+                    total = 40 + pl;
+                    good = pl != 0 && total <= avail && pe_l4(true, 6, proto, b + 40, pl);
+                }
+                // l3_len is 16 bits: an IPv6 packet above 65535 B (payloadLength > 65495) cannot be
+                // described (it never fits a umem frame); refused
+                if (good && total <= 0xffff) {
+                    d.l3_off = o + hl; d.l3_len = (uint16_t)total; d.l4_off = (uint16_t)l4o;
+                    d.l3_ver = 6; d.l4_proto = (uint8_t)proto;
+                    st = 0;
                 }
             }
         }

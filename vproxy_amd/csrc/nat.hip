@@ -1,0 +1,388 @@
+// nat.hip -- K5 of libvpcsum (gfx950): NAT / TTL rewrites with the checksum update, in place.
+//
+// Java writes the new bytes through the setters and marks the sums dirty, and the next
+// getRawPacket(0) recomputes the dirty sums in full:
+//   SwitchUtils.applyNat                   core/.../vswitch/util/SwitchUtils.java:522-542
+//   Ipv4Packet.setSrc / setDst / setTtl    base/.../vpacket/Ipv4Packet.java:401-407, 433-458
+//     pseudoHeaderChanges (TCP / UDP)      Ipv4Packet.java:236-240
+//   Ipv6Packet.setSrc / setDst             Ipv6Packet.java:374-396 (setHopLimit :354-359 marks
+//     pseudoHeaderChanges (ICMP, TCP, UDP) nothing dirty: no sum covers the hop limit)
+//                                          Ipv6Packet.java:238-242
+//   TcpPacket / UdpPacket.setSrcPort / setDstPort  TcpPacket.java:31-51, UdpPacket.java:188-209
+// RFC 1624 eqn. 3, HC' = ~(~HC + ~m + m'), is bit-identical to that full recompute whenever the
+// incoming checksum is correct; UDP with stored 0 is recomputed in full.
+// VPCSUM_NAT_STRICT_JAVA rewrites only and hands the dirty flags to the checksum kernel, which
+// recomputes in full: identical to Java for any input.
+//
+// Two rewrite-entry formats: vpcsum_nat4_t (16 B, IPv4 only: BASELINE config C5's 72 B/packet)
+// and vpcsum_nat_t (48 B, IPv4 and IPv6).  One lane per packet.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "vpcsum.h"
+#include "internal.h"
+#include "device_common.h"
+
+namespace vpcsum {
+
+// One packet's rewrite, decoded from either entry format.  Address bytes stay in load order
+// (byte i of the address = byte i & 3 of word i >> 2).
+struct NatRw {
+    uint32_t src[4], dst[4];
+    uint32_t ports;   // bytes 0..1 source port, 2..3 destination port (network order)
+    int mask, ttl;
+};
+
+__device__ __forceinline__ NatRw nat_rw4(const uint4 q) {
+    NatRw r;
+    r.src[0] = q.x; r.dst[0] = q.y;
+    r.src[1] = r.src[2] = r.src[3] = r.dst[1] = r.dst[2] = r.dst[3] = 0;
+    r.ports = q.z;
+    r.mask = (int)(q.w & 0xff);
+    r.ttl = (int)((q.w >> 8) & 0xff);   // rsv[0]: the VPCSUM_NAT_SET_TTL value
+    return r;
+}
+__device__ __forceinline__ NatRw nat_rw6(const uint4 a, const uint4 b, const uint4 c) {
+    NatRw r;
+    r.src[0] = a.x; r.src[1] = a.y; r.src[2] = a.z; r.src[3] = a.w;
+    r.dst[0] = b.x; r.dst[1] = b.y; r.dst[2] = b.z; r.dst[3] = b.w;
+    r.ports = c.x;
+    r.mask = (int)(c.y & 0xff);
+    r.ttl = (int)((c.y >> 8) & 0xff);
+    return r;
+}
+// big-endian 16-bit word k (bytes 2k, 2k+1) of an address / of the port pair
+__device__ __forceinline__ uint32_t rw_word(const uint32_t* a, int k) {
+    const uint32_t w = a[k >> 1] >> ((k & 1) * 16);
+    return ((w & 0xff) << 8) | ((w >> 8) & 0xff);
+}
+
+// What a packet's rewrite did: RFC 1624 differences (sums of ~m + m'), Java's dirty flags, and the
+// byte range [lo, hi) (relative to the L3 start) that changed.
+struct NatAcc {
+    uint32_t ip_diff, l4_diff;
+    bool ip_dirty, l4_dirty, l4_touch;
+    int lo, hi;
+};
+
+__device__ __forceinline__ void nat_word(uint8_t* w, int q, uint32_t mn, uint32_t& d1, uint32_t* d2) {
+    const uint32_t m = ((uint32_t)w[q] << 8) | w[q + 1];
+    d1 += (~m & 0xffff) + mn;
+    if (d2) *d2 += (~m & 0xffff) + mn;
+    w[q] = (uint8_t)(mn >> 8);
+    w[q + 1] = (uint8_t)mn;
+}
+__device__ __forceinline__ void grow(NatAcc& a, int lo, int hi) {
+    a.lo = min(a.lo, lo);
+    a.hi = max(a.hi, hi);
+}
+
+// The setters on the packet whose L3 header is w[0..len) (w: an LDS window or the frame itself).
+// l4sum: the L4 checksum field exists (the segment holds it).
+__device__ __forceinline__ NatAcc nat_setters(uint8_t* w, int ver, int proto, int len, int l4o, bool l4sum,
+                                             const NatRw& r) {
+    NatAcc a = {0u, 0u, false, false, false, 1 << 20, 0};
+    // which L4 sums the pseudo-header addresses dirty: TCP / UDP under IPv4, also ICMP / ICMPv6
+    // under IPv6; an ICMPv4 message has no pseudo header, so its sum does not change
+    const bool addr_dirty = l4sum && (proto == 6 || proto == 17 || (ver == 6 && (proto == 58 || proto == 1)));
+    const bool addr_sum = addr_dirty && proto != 1;
+    uint32_t* l4d = addr_sum ? &a.l4_diff : nullptr;
+    if (ver == 4) {
+        if (r.mask & VPCSUM_NAT_SRC) {
+            for (int k = 0; k < 2; ++k) nat_word(w, 12 + 2 * k, rw_word(r.src, k), a.ip_diff, l4d);
+            a.ip_dirty = true; a.l4_dirty |= addr_dirty; a.l4_touch |= addr_sum;
+            grow(a, 12, 16);
+        }
+        if (r.mask & VPCSUM_NAT_DST) {
+            for (int k = 0; k < 2; ++k) nat_word(w, 16 + 2 * k, rw_word(r.dst, k), a.ip_diff, l4d);
+            a.ip_dirty = true; a.l4_dirty |= addr_dirty; a.l4_touch |= addr_sum;
+            grow(a, 16, 20);
+        }
+        if (r.mask & VPCSUM_NAT_SET_TTL) {   // setTtl(ttl)
+            nat_word(w, 8, ((uint32_t)r.ttl << 8) | w[9], a.ip_diff, nullptr);
+            a.ip_dirty = true;
+            grow(a, 8, 9);
+        }
+        if (r.mask & VPCSUM_NAT_DEC_TTL) {   // IPInputRoute: setTtl(ttl - 1)
+            nat_word(w, 8, ((uint32_t)((w[8] - 1) & 0xff) << 8) | w[9], a.ip_diff, nullptr);
+            a.ip_dirty = true;
+            grow(a, 8, 9);
+        }
+    } else {
+        uint32_t none = 0;
+        if (r.mask & VPCSUM_NAT_SRC) {
+            for (int k = 0; k < 8; ++k) nat_word(w, 8 + 2 * k, rw_word(r.src, k), none, l4d);
+            a.l4_dirty |= addr_dirty; a.l4_touch |= addr_sum;
+            grow(a, 8, 24);
+        }
+        if (r.mask & VPCSUM_NAT_DST) {
+            for (int k = 0; k < 8; ++k) nat_word(w, 24 + 2 * k, rw_word(r.dst, k), none, l4d);
+            a.l4_dirty |= addr_dirty; a.l4_touch |= addr_sum;
+            grow(a, 24, 40);
+        }
+        if (r.mask & VPCSUM_NAT_SET_TTL) { w[7] = (uint8_t)r.ttl; grow(a, 7, 8); }          // setHopLimit
+        if (r.mask & VPCSUM_NAT_DEC_TTL) { w[7] = (uint8_t)(w[7] - 1); grow(a, 7, 8); }
+    }
+    if (l4sum && (proto == 6 || proto == 17)) {
+        if (r.mask & VPCSUM_NAT_SPORT) {
+            nat_word(w, l4o, rw_word(&r.ports, 0), a.l4_diff, nullptr);
+            a.l4_dirty = a.l4_touch = true;
+            grow(a, l4o, l4o + 2);
+        }
+        if (r.mask & VPCSUM_NAT_DPORT) {
+            nat_word(w, l4o + 2, rw_word(&r.ports, 1), a.l4_diff, nullptr);
+            a.l4_dirty = a.l4_touch = true;
+            grow(a, l4o + 2, l4o + 4);
+        }
+    }
+    return a;
+}
+
+// RFC 1624 eqn. 3 on the fields of w.  Returns true when the L4 sum is a UDP "no checksum" (stored
+// 0): Java recomputes it in full (UdpPacket.java:136-164), done by nat_udp_full once the rewritten
+// header is in memory.
+__device__ __forceinline__ bool nat_rfc1624(uint8_t* w, int proto, int l4o, int fld, NatAcc& a) {
+    if (a.ip_dirty) {
+        const uint32_t hc = ((uint32_t)w[10] << 8) | w[11];
+        const uint32_t c = ~fold32((~hc & 0xffff) + fold32(a.ip_diff)) & 0xffff;
+        w[10] = (uint8_t)(c >> 8); w[11] = (uint8_t)c;
+        grow(a, 10, 12);
+    }
+    if (a.l4_touch) {
+        const int f = l4o + fld;
+        const uint32_t hc = ((uint32_t)w[f] << 8) | w[f + 1];
+        if (proto == 17 && hc == 0) return true;
+        uint32_t c = ~fold32((~hc & 0xffff) + fold32(a.l4_diff)) & 0xffff;
+        if (proto == 17 && c == 0) c = 0xffff;
+        w[f] = (uint8_t)(c >> 8); w[f + 1] = (uint8_t)c;
+        grow(a, f, f + 2);
+    }
+    return false;
+}
+
+// Folded LE-absolute sum of bytes [lo, hi) (absolute addresses) minus a 2-byte field, one lane.
+__device__ uint32_t lane_sum_range(const uint8_t* lo_p, const uint8_t* hi_p, const uint8_t* fld_p) {
+    const uintptr_t lo = (uintptr_t)lo_p, hi = (uintptr_t)hi_p, fa = (uintptr_t)fld_p;
+    const uintptr_t a = lo & ~(uintptr_t)3;
+    uint64_t acc = 0;
+    for (uintptr_t d = a; d < hi; d += 4) {
+        const uint32_t v = *(const __attribute__((address_space(1))) uint32_t*)d;
+        const int rd = (int)(d - a);
+        uint32_t m = bmask(rd, (int)(lo - a), (int)(hi - a));
+        if (fld_p) m &= ~bmask(rd, (int)(fa - a), (int)(fa - a) + 2);
+        acc += v & m;
+    }
+    return fold64(acc);
+}
+
+// Full UDP recompute from memory (the stored-0 case): pseudo header (IPv4 12..20 / IPv6 8..40,
+// proto 17, the L4 length as 16 / 32 bits) + the segment with the field excluded.
+__device__ void nat_udp_full(uint8_t* l3, int ver, int len, int l4o) {
+    uint8_t* l4p = l3 + l4o;
+    const uint32_t seg = orient(lane_sum_range(l4p, l3 + len, l4p + 6), (int)((uintptr_t)l4p & 1));
+    const uint32_t ps = orient(lane_sum_range(l3 + (ver == 4 ? 12 : 8), l3 + (ver == 4 ? 20 : 40), nullptr),
+                               (int)((uintptr_t)l3 & 1));
+    const uint32_t l4len = (uint32_t)(len - l4o);
+    uint32_t c = 0xffff - fold32(seg + ps + 17u + (l4len & 0xffff) + (l4len >> 16));
+    if (c == 0) c = 0xffff;
+    st16(l4p + 6, c);
+}
+
+// Descriptor checks shared by both kernels; fmt 0 entries carry IPv4 addresses only.
+__device__ __forceinline__ bool nat_desc_ok(uint64_t off, int len, int l4o, int ver, uint64_t arena_len, int fmt) {
+    if (off > arena_len || (uint64_t)len > arena_len - off) return false;
+    if (ver == 4) return len >= 20 && l4o >= 20 && l4o <= len && !(l4o & 3);
+    if (ver == 6) return fmt == 1 && len >= 40 && l4o >= 40 && l4o <= len;
+    return false;
+}
+__device__ __forceinline__ bool nat_l4sum(int ver, int proto, int len, int l4o) {
+    const int fld = l4_field(proto);
+    return fld >= 0 && !(ver == 4 && proto == 58) && len - l4o >= fld + 2;
+}
+
+template <int FMT>
+__device__ __forceinline__ NatRw nat_load_rw(const void* rw, uint32_t p) {
+    if (FMT == 0) return nat_rw4(((const uint4*)rw)[p]);
+    const uint4* q = (const uint4*)rw + 3 * (size_t)p;
+    return nat_rw6(q[0], q[1], q[2]);
+}
+
+// One packet with byte accesses straight on the frame (IPv4 options / IPv6 extension headers
+// beyond the wide window, arenas the buffer path cannot address, or nat_mode bit 8).
+template <int FMT>
+__device__ void nat_scalar(uint8_t* __restrict__ arena, uint64_t arena_len, const uint4 dv, const NatRw& r, uint32_t p,
+                           uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out, bool strict) {
+    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+    const int len = dv.z & 0xffff, l4o = dv.z >> 16;
+    const int ver = dv.w & 0xff, proto = (dv.w >> 8) & 0xff;
+    if (!nat_desc_ok(off, len, l4o, ver, arena_len, FMT)) {
+        if (status) status[p] = VPCSUM_S_BAD_DESC;
+        if (flags_out) flags_out[p] = kFlagRejected;
+        return;
+    }
+    uint8_t* l3 = arena + off;
+    const bool l4sum = nat_l4sum(ver, proto, len, l4o);
+    NatAcc a = nat_setters(l3, ver, proto, len, l4o, l4sum, r);
+    if (strict) {
+        if (flags_out) flags_out[p] = (a.ip_dirty ? VPCSUM_F_IP : 0) | (a.l4_dirty ? VPCSUM_F_L4 : 0);
+        return;
+    }
+    if (nat_rfc1624(l3, proto, l4o, l4_field(proto), a)) nat_udp_full(l3, ver, len, l4o);
+    if (status) status[p] = VPCSUM_S_DONE;
+}
+
+template <int FMT>
+__global__ __launch_bounds__(256) void k_nat(uint8_t* __restrict__ arena, uint64_t arena_len,
+                                            const uint4* __restrict__ desc, const void* __restrict__ rw, uint32_t n,
+                                            uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out, int strict) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x)
+        nat_scalar<FMT>(arena, arena_len, desc[p], nat_load_rw<FMT>(rw, p), p, status, flags_out, strict != 0);
+}
+
+// Wide form: the window [align16(L3), align16(L3) + 96) holding every byte a rewrite touches --
+// the header, the ports and the L4 checksum field of IPv4 with options or IPv6 without extension
+// headers -- is read with up to six 16-B buffer loads (only the chunks the packet needs), staged
+// in this lane's LDS slot, rewritten there with byte-addressed LDS ops (the window's offset
+// differs per packet), and the changed range is stored back as ONE run of dwordx4 / x2 / dword
+// stores (bytewise only where it would pass the packet end: the next bytes may be another
+// packet's).  W packets per lane and iteration keep W windows in flight.
+constexpr int kNatChunks = 6;                   // window: 96 B
+constexpr int kNatSlotDw = 4 * kNatChunks + 1;  // LDS slot per lane: an odd dword stride (no bank conflicts)
+
+template <int FMT, bool STRICT, int W>
+__global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint64_t arena_len,
+                                             const uint4* __restrict__ desc, const void* __restrict__ rw, uint32_t n,
+                                             uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    __shared__ uint32_t s_win[256 * kNatSlotDw];
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
+    uint32_t* slot = &s_win[threadIdx.x * kNatSlotDw];
+    uint8_t* w = (uint8_t*)slot;
+    const uint32_t T = gridDim.x * blockDim.x;
+    for (uint32_t p0 = blockIdx.x * blockDim.x + threadIdx.x; p0 < n; p0 += W * T) {
+        uint4 dv[W];
+        NatRw rr[W];
+        int wend[W];
+        uint4 v[W][kNatChunks];
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            dv[i] = p < n ? desc[p] : make_uint4(0, 0, 0, 0);
+            rr[i] = nat_load_rw<FMT>(rw, p < n ? p : 0);
+        }
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
+            const int len = dv[i].z & 0xffff, l4o = dv[i].z >> 16;
+            const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
+            const int r0 = (int)(off & 15);
+            int need = ver == 4 ? 20 : 40;
+            if (nat_l4sum(ver, proto, len, l4o)) need = max(need, l4o + l4_field(proto) + 2);
+            wend[i] = p < n && nat_desc_ok(off, len, l4o, ver, arena_len, FMT) && r0 + need <= 16 * kNatChunks
+                          ? r0 + need : 0;   // 0: the packet takes the byte-access path
+            const uint32_t boff = (uint32_t)(off - (uint64_t)r0);
+#pragma unroll
+            for (int k = 0; k < kNatChunks; ++k) {
+                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (k << 4) < wend[i] ? boff + (k << 4) : kOutOfRange, 0, 0);
+                v[i][k] = make_uint4(x.x, x.y, x.z, x.w);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            if (p >= n) continue;
+            if (!wend[i]) {
+                nat_scalar<FMT>(arena, arena_len, dv[i], rr[i], p, status, flags_out, STRICT);
+                continue;
+            }
+            const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
+            const int len = dv[i].z & 0xffff, l4o = dv[i].z >> 16;
+            const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
+            const int r0 = (int)(off & 15);
+            const uint32_t boff = (uint32_t)(off - (uint64_t)r0);
+#pragma unroll
+            for (int k = 0; k < kNatChunks; ++k) {
+                if ((k << 4) < wend[i]) {
+                    slot[4 * k] = v[i][k].x; slot[4 * k + 1] = v[i][k].y;
+                    slot[4 * k + 2] = v[i][k].z; slot[4 * k + 3] = v[i][k].w;
+                }
+            }
+            uint8_t* l3w = w + r0;
+            NatAcc a = nat_setters(l3w, ver, proto, len, l4o, nat_l4sum(ver, proto, len, l4o), rr[i]);
+            const bool udp_zero = !STRICT && nat_rfc1624(l3w, proto, l4o, l4_field(proto), a);
+            // store back [lo, hi) of the packet as one run of dwords, widest first
+            if (a.hi > a.lo) {
+                const int lim = r0 + len;
+                int j = (r0 + a.lo) >> 2;
+                const int je = (r0 + a.hi + 3) >> 2;
+                const int jfull = lim >> 2;   // dwords below this lie inside the packet
+                typedef __attribute__((address_space(1))) uint32_t g32;
+                while (j < je) {
+                    uint8_t* dst = arena + boff + 4 * j;
+                    if (!(j & 3) && j + 4 <= je && j + 4 <= jfull) {
+                        const v4u q = {slot[j], slot[j + 1], slot[j + 2], slot[j + 3]};
+                        *(__attribute__((address_space(1))) v4u*)dst = q;
+                        j += 4;
+                    } else if (!(j & 1) && j + 2 <= je && j + 2 <= jfull) {
+                        typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+                        const v2u q = {slot[j], slot[j + 1]};
+                        *(__attribute__((address_space(1))) v2u*)dst = q;
+                        j += 2;
+                    } else if (j + 1 <= jfull) {
+                        *(g32*)dst = slot[j];
+                        j += 1;
+                    } else {
+                        for (int q = 4 * j; q < lim; ++q) arena[boff + q] = w[q];
+                        j += 1;
+                    }
+                }
+            }
+            if (STRICT) {
+                if (flags_out) flags_out[p] = (a.ip_dirty ? VPCSUM_F_IP : 0) | (a.l4_dirty ? VPCSUM_F_L4 : 0);
+                continue;
+            }
+            if (udp_zero) nat_udp_full(arena + off, ver, len, l4o);
+            if (status) status[p] = VPCSUM_S_DONE;
+        }
+    }
+}
+
+constexpr int kNatWideLog2 = 1;   // packets per lane and iteration of k_natw: 2
+
+hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw, int fmt,
+                      uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const bool strict = (nat_mode & VPCSUM_NAT_STRICT_JAVA) != 0;
+    // nat_mode bits 12..14 (internal tuning): log2 packets per lane and iteration of the wide
+    // kernel + 1 (0 = default)
+    const int wsel = (int)((nat_mode >> 12) & 7u);
+    const int wl2 = wsel ? (wsel - 1 > 2 ? 2 : wsel - 1) : kNatWideLog2;
+    // one iteration of W packets per lane covers the batch when the chip holds the grid
+    uint32_t g = (n + (256u << wl2) - 1) / (256u << wl2);
+    const uint32_t cap = (uint32_t)num_cus(dev) * 8;
+    if (g > cap) g = cap;
+    // nat_mode bit 8 (internal tuning): force the byte-access kernel
+    const bool wide = !(nat_mode & 0x100u) && arena_len <= kMaxBufArena && !((uintptr_t)arena & 15);
+    const uint4* d = (const uint4*)desc;
+    if (wide) {
+#define VPC_NAT(F, S, W) hipLaunchKernelGGL((k_natw<F, S, W>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out)
+#define VPC_NAT_W(F, S) do { if (wl2 == 0) VPC_NAT(F, S, 1); else if (wl2 == 1) VPC_NAT(F, S, 2); else VPC_NAT(F, S, 4); } while (0)
+        if (fmt == 0) {
+            if (strict) VPC_NAT_W(0, true); else VPC_NAT_W(0, false);
+        } else {
+            if (strict) VPC_NAT_W(1, true); else VPC_NAT_W(1, false);
+        }
+#undef VPC_NAT_W
+#undef VPC_NAT
+    } else if (fmt == 0) {
+        hipLaunchKernelGGL(k_nat<0>, dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out, strict ? 1 : 0);
+    } else {
+        hipLaunchKernelGGL(k_nat<1>, dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out, strict ? 1 : 0);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace vpcsum

@@ -48,6 +48,18 @@ def max_over_ranks(x: float) -> float:
     return float(t.item())
 
 
+def sum_over_ranks(x: float) -> float:
+    """Sum of a float over all ranks (bench: algorithmic bytes of all shards); identity without
+    torch.distributed."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(x)
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def all_ranks_ok(ok: bool) -> bool:
     """True only if every rank reports ok (bench verify gate)."""
     import torch
