@@ -237,7 +237,9 @@ int vpcsum_ctx_nat_submit(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena_le
                           const vpcsum_desc_t* h_desc, const vpcsum_nat_t* h_rw, uint32_t n,
                           uint8_t* h_status, uint32_t nat_mode, uint64_t* ticket);
 /* Pipelined host->device->host throughput helper: processes a host arena of n fixed-stride
- * frames in `chunks` double-buffered pieces over two streams (H2D || kernel || D2H). */
+ * frames in `chunks` double-buffered pieces over two streams (H2D || kernel || D2H).  The arena,
+ * descriptors and h_out must be registered (page-locked); with VPCSUM_MODE_WRITE the checksum
+ * fields are also stored into the host frames (through the arena's mapping). */
 int vpcsum_ctx_pipeline(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint32_t stride, uint32_t copy_bytes,
                         const vpcsum_desc_t* h_desc, uint32_t n, uint32_t* h_out,
                         uint32_t mode, uint32_t chunks);
@@ -249,13 +251,13 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint32_t stride, ui
 typedef struct PNIException_vpcsum {
     char*   type;
     char    message[4096];
-    int32_t errno_;
-} PNIException_vpcsum;
+    int32_t errno_;    /* EINVAL (IllegalArgumentException) / EIO (IOException) on a throw */
+} PNIException_vpcsum;   /* sizeof 4112: message at 8, errno_ at 4104 (tests/cpp/pni_layout.c) */
 
 typedef struct PNIEnv_vpcsum_long {
     PNIException_vpcsum ex;
     union { int64_t return_; struct { uint64_t a, b; } placeholder_; };
-} PNIEnv_vpcsum_long;
+} PNIEnv_vpcsum_long;   /* sizeof 4128, return_ at 4112: PNIEnv_long of pni.h */
 
 typedef struct PNIEnv_vpcsum_int {
     PNIException_vpcsum ex;

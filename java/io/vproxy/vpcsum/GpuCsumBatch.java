@@ -5,8 +5,8 @@ import io.vproxy.vpacket.AbstractIpPacket;
 import io.vproxy.vpacket.EthernetPacket;
 import io.vproxy.vpacket.IcmpPacket;
 import io.vproxy.vpacket.Ipv4Packet;
-import io.vproxy.vpacket.TcpPacket;
-import io.vproxy.vpacket.UdpPacket;
+import io.vproxy.vpxdp.ChunkInfo;
+import io.vproxy.vpxdp.XDPConsts;
 import io.vproxy.vswitch.PacketBuffer;
 
 import java.io.IOException;
@@ -19,8 +19,8 @@ import java.lang.foreign.ValueLayout;
  *
  * Egress is the flag-and-flush contract the XDP path already has with its native code
  * (SwitchUtils.checksumFlagsFor, SwitchUtils.java:297-316; XDPIface.sendPacket / completeTx,
- * XDPIface.java:100-178, 227-243): {@link #defer} records which sums of a frame are dirty instead
- * of setting VP_CSUM_* on the chunk, {@link #flush} (called at the top of Iface.completeTx, before
+ * XDPIface.java:100-178, 227-243): {@link #defer} takes over the VP_CSUM_* work of a frame instead
+ * of leaving it to the native path, {@link #flush} (called at the top of Iface.completeTx, before
  * xsk.writePackets) computes every deferred sum in one GPU pass (the resident service grid for
  * flushes of up to 512 frames, a launch above that) and writes the results into the frames
  * (MODE_WRITE), byte-for-byte what getRawPacket(0) would have produced
@@ -45,7 +45,13 @@ public final class GpuCsumBatch implements AutoCloseable {
     private final MemorySegment out;
     private final MemorySegment status;
     private final int capacity;
+    private final ChunkInfo[] chunks;
+    private final int[] nativeFlagsOf;
     private int n = 0;
+
+    /** Flushes of fewer frames go back to the native VP_CSUM_* path (the GPU breaks even at about
+     * 5 frames per flush with the service grid, DESIGN.md §8). */
+    public static final int SMALL_FLUSH = 5;
 
     public GpuCsumBatch(int device, MemorySegment umem, int capacity) throws IOException {
         this.umem = umem;
@@ -58,6 +64,8 @@ public final class GpuCsumBatch implements AutoCloseable {
         this.desc = arena.allocate((long) DESC * capacity, 16);
         this.out = arena.allocate(4L * capacity, 16);
         this.status = arena.allocate(capacity, 16);
+        this.chunks = new ChunkInfo[capacity];
+        this.nativeFlagsOf = new int[capacity];
     }
 
     public boolean isFull() {
@@ -65,38 +73,39 @@ public final class GpuCsumBatch implements AutoCloseable {
     }
 
     /**
-     * Record the dirty checksums of {@code pkb}, whose frame lies in the umem at byte offset
-     * {@code frameOff} (chunk address + pkb.pktOff).  Returns false when nothing is dirty (the
-     * caller then sends the frame as is), true when the frame is now owned by the batch until
-     * {@link #flush}.  Mirrors SwitchUtils.checksumFlagsFor: IP dirty -> VP_CSUM_IP, upper layer
-     * dirty -> VP_CSUM_UP.
+     * Take over the dirty checksums of {@code pkb}, whose Ethernet frame lies in the umem at byte
+     * offset {@code frameOff} in {@code chunk} (the zero-copy branch of XDPIface.sendPacket:
+     * chunk.getAddr() + pkb.pktOff; the copying branch: the pktaddr the frame was copied to).
+     * {@code nativeFlags} is what SwitchUtils.checksumFlagsFor (SwitchUtils.java:297-316) returned
+     * for the packet: VP_CSUM_IP -> F_IP, VP_CSUM_UP -> F_L4, VP_CSUM_UP_PSEUDO -> F_L4P (the GPU
+     * writes the pseudo-header sum, the NIC completes it; an ICMPv4 message has no pseudo header,
+     * so it stays with the native path).  Returns the flags the chunk must carry now:
+     * VP_CSUM_XDP_OFFLOAD (and the ICMPv4 pseudo request) stay, the rest is the GPU's.  A flush
+     * below {@link #SMALL_FLUSH} frames hands every deferred frame back to the native path instead
+     * (its full nativeFlags are restored on the chunk): a GPU round trip costs more than the CPU
+     * there (DESIGN.md §8).
      */
-    public boolean defer(PacketBuffer pkb, long frameOff) {
-        return defer(pkb, frameOff, false);
-    }
-
-    /**
-     * As {@link #defer(PacketBuffer, long)}; with {@code offload} (the TX queue completes L4
-     * checksums: VP_CSUM_UP_PSEUDO | VP_CSUM_XDP_OFFLOAD) the upper layer gets only its
-     * pseudo-header sum (F_L4P), ICMPv4 (no pseudo header) its full sum.
-     */
-    public boolean defer(PacketBuffer pkb, long frameOff, boolean offload) {
-        if (!(pkb.pkt.getPacket() instanceof AbstractIpPacket ip)) {
-            return false;
+    public int defer(PacketBuffer pkb, ChunkInfo chunk, long frameOff, int nativeFlags) {
+        if (nativeFlags == 0 || !(pkb.pkt.getPacket() instanceof AbstractIpPacket ip)) {
+            return nativeFlags;
         }
         int flags = 0;
-        if (ip instanceof Ipv4Packet && ip.isRequireUpdatingChecksum()) {
+        int keep = nativeFlags & XDPConsts.VP_CSUM_XDP_OFFLOAD;
+        if ((nativeFlags & XDPConsts.VP_CSUM_IP) != 0) {
             flags |= VPCsum.F_IP;
         }
-        // a pseudo-header change (setSrc/setDst) already marked TCP/UDP dirty through
-        // pseudoHeaderChanges() (Ipv4Packet.java:236-240, Ipv6Packet.java:238-242)
-        var upper = ip.getPacket();
-        boolean l4Kind = upper instanceof TcpPacket || upper instanceof UdpPacket || upper instanceof IcmpPacket;
-        if (l4Kind && upper.isRequireUpdatingChecksum()) {
-            flags |= (offload && !(upper instanceof IcmpPacket icmp && !icmp.isIpv6())) ? VPCsum.F_L4P : VPCsum.F_L4;
+        if ((nativeFlags & XDPConsts.VP_CSUM_UP) != 0) {
+            flags |= VPCsum.F_L4;
+        }
+        if ((nativeFlags & XDPConsts.VP_CSUM_UP_PSEUDO) != 0) {
+            if (ip.getPacket() instanceof IcmpPacket icmp && !icmp.isIpv6()) {
+                keep |= XDPConsts.VP_CSUM_UP_PSEUDO;
+            } else {
+                flags |= VPCsum.F_L4P;
+            }
         }
         if (flags == 0) {
-            return false;
+            return nativeFlags;
         }
         if (n == capacity) {
             throw new IllegalStateException("batch full: flush first");
@@ -111,20 +120,50 @@ public final class GpuCsumBatch implements AutoCloseable {
         desc.set(ValueLayout.JAVA_BYTE, d + 13, (byte) ip.getProtocol());
         desc.set(ValueLayout.JAVA_BYTE, d + 14, (byte) flags);
         desc.set(ValueLayout.JAVA_BYTE, d + 15, (byte) 0);
+        chunks[n] = chunk;
+        nativeFlagsOf[n] = nativeFlags;
         ++n;
-        return true;
+        return keep;
     }
 
-    /** Compute and write every deferred checksum into its frame; call before xsk.writePackets. */
+    /**
+     * Compute and write every deferred checksum into its frame; call at the top of
+     * Iface.completeTx, before xsk.writePackets.  Returns the frames the GPU handled (0 when a
+     * small flush went back to the native path).
+     */
     public int flush() throws IOException {
         if (n == 0) {
             return 0;
         }
+        int done = n;
+        if (n < SMALL_FLUSH) {
+            for (int i = 0; i < n; ++i) {
+                chunks[i].setCsumFlags(nativeFlagsOf[i]);
+                chunks[i] = null;
+            }
+            n = 0;
+            return 0;
+        }
         long t = VPCsum.get().submit(env, ctx, umem, umemLen, desc, n, out, status, VPCsum.MODE_WRITE);
         VPCsum.get().waitFor(env, ctx, t);
-        int done = n;
+        for (int i = 0; i < n; ++i) {
+            chunks[i] = null;
+        }
         n = 0;
         return done;
+    }
+
+    /**
+     * SwitchUtils.applyNat for a batch of frames in the umem (SwitchUtils.java:522-542): each
+     * 48-byte entry of {@code rw} (addresses, ports, TTL / hop limit; VPCsum.NAT_*) rewrites the
+     * packet of the matching descriptor of {@code natDesc} in place, checksums updated as the
+     * setters + getRawPacket(0) would leave them.  Returns one status byte per packet.
+     */
+    public MemorySegment nat(MemorySegment natDesc, MemorySegment rw, int count, boolean strictJava) throws IOException {
+        long t = VPCsum.get().natSubmit(env, ctx, umem, umemLen, natDesc, rw, count, status,
+            strictJava ? VPCsum.NAT_STRICT_JAVA : VPCsum.NAT_RFC1624);
+        VPCsum.get().waitFor(env, ctx, t);
+        return status;
     }
 
     /**

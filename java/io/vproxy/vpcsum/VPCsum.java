@@ -11,9 +11,14 @@ import java.lang.invoke.MethodHandle;
  * Downcalls into libvpcsum.so (MI355X batched Internet checksum), written in the shape the PNI
  * generator emits for the existing natives (compare
  * base/src/main/generated/io/vproxy/vfd/posix/PosixNative.java:729-744 in vproxy): one
- * critical (non-blocking, no upcall) downcall per method, exceptions travel through the PNIEnv
- * (0 = ok, -1 = exception stored in ENV).  The C side is include/vpcsum.h, symbols
- * Java_io_vproxy_vpcsum_VPCsum_*.
+ * downcall per method, exceptions travel through the PNIEnv (0 = ok, -1 = exception stored in
+ * ENV).  The C side is include/vpcsum.h, symbols Java_io_vproxy_vpcsum_VPCsum_*.
+ *
+ * No method is linked critical ({@code setCritical(false)} throughout): every entry point may
+ * block -- create / registerArena allocate and page-lock through the HIP runtime, submit /
+ * natSubmit / verifyFrames finish the batch that last used their slot (an event wait, or the
+ * service grid's completion), waitFor and setService wait by design.  A critical downcall keeps
+ * the thread in Java state and would stall every safepoint (GC included) for that long.
  *
  * Load the library the same way vproxy loads its other natives:
  * {@code Utils.loadDynamicLibrary("vpcsum")} (base/src/main/java/io/vproxy/base/util/Utils.java:1014-1030).
@@ -46,8 +51,19 @@ public class VPCsum {
     public static final int MODE_COMPUTE = 0x00;
     public static final int MODE_VERIFY = 0x01;
     public static final int MODE_WRITE = 0x10;
+    // NAT / TTL rewrite masks (vpcsum_nat_t.mask) and modes
+    public static final int NAT_SRC = 0x01;
+    public static final int NAT_DST = 0x02;
+    public static final int NAT_SPORT = 0x04;
+    public static final int NAT_DPORT = 0x08;
+    public static final int NAT_DEC_TTL = 0x10;
+    public static final int NAT_SET_TTL = 0x20;
+    public static final int NAT_RFC1624 = 0x00;
+    public static final int NAT_STRICT_JAVA = 0x01;
+    /** bytes of one vpcsum_nat_t rewrite entry: src[16] dst[16] sport[2] dport[2] mask ttl rsv[10] */
+    public static final int NAT_ENTRY = 48;
 
-    private static final MethodHandle createMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(true),
+    private static final MethodHandle createMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
         "Java_io_vproxy_vpcsum_VPCsum_create", int.class /* device */, long.class /* maxArena */, int.class /* maxPkts */);
 
     /** Create a context on GPU {@code device}: device buffers for one batch of up to maxPkts
@@ -67,7 +83,7 @@ public class VPCsum {
         return ENV.returnLong();
     }
 
-    private static final MethodHandle registerArenaMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(true),
+    private static final MethodHandle registerArenaMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
         "Java_io_vproxy_vpcsum_VPCsum_registerArena", long.class /* ctx */, MemorySegment.class /* arena */, long.class /* len */);
 
     /** Page-lock a long-lived arena (an AF_XDP umem, UMem.java:36-44) once, so batches from it
@@ -86,7 +102,7 @@ public class VPCsum {
         }
     }
 
-    private static final MethodHandle submitMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(true),
+    private static final MethodHandle submitMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
         "Java_io_vproxy_vpcsum_VPCsum_submit", long.class /* ctx */, MemorySegment.class /* arena */, long.class /* arenaLen */,
         MemorySegment.class /* desc */, int.class /* n */, MemorySegment.class /* out */, MemorySegment.class /* status */,
         int.class /* mode */);
@@ -113,7 +129,7 @@ public class VPCsum {
         "Java_io_vproxy_vpcsum_VPCsum_waitFor", long.class /* ctx */, long.class /* ticket */);
 
     /** Block until the batch of {@code ticket} is done; results (and, with MODE_WRITE, the
-     * checksum fields inside the frames) are valid afterwards. Not critical: it may block. */
+     * checksum fields inside the frames) are valid afterwards. */
     public void waitFor(PNIEnv ENV, long ctx, long ticket) throws java.io.IOException {
         ENV.reset();
         int ERR;
@@ -128,7 +144,7 @@ public class VPCsum {
         }
     }
 
-    private static final MethodHandle verifyFramesMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(true),
+    private static final MethodHandle verifyFramesMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
         "Java_io_vproxy_vpcsum_VPCsum_verifyFrames", long.class /* ctx */, MemorySegment.class /* arena */,
         long.class /* arenaLen */, MemorySegment.class /* frameOff */, MemorySegment.class /* frameLen */, int.class /* n */,
         MemorySegment.class /* out */, MemorySegment.class /* status */);
@@ -154,13 +170,40 @@ public class VPCsum {
         return ENV.returnLong();
     }
 
+    private static final MethodHandle natSubmitMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
+        "Java_io_vproxy_vpcsum_VPCsum_natSubmit", long.class /* ctx */, MemorySegment.class /* arena */,
+        long.class /* arenaLen */, MemorySegment.class /* desc */, MemorySegment.class /* rw */, int.class /* n */,
+        MemorySegment.class /* status */, int.class /* natMode */);
+
+    /** SwitchUtils.applyNat for a batch (SwitchUtils.java:522-542): rewrite {@code rw[i]}
+     * (48-byte vpcsum_nat_t entries: addresses, ports, TTL / hop limit) into the packet of
+     * {@code desc[i]} in place, with the checksums updated as getRawPacket(0) would recompute them
+     * (NAT_RFC1624 on valid input, NAT_STRICT_JAVA for any input).  Frames in the registered umem
+     * are rewritten where they lie.  status[i]: S_DONE or S_BAD_DESC.  Returns a ticket for
+     * {@link #waitFor}. */
+    public long natSubmit(PNIEnv ENV, long ctx, MemorySegment arena, long arenaLen, MemorySegment desc,
+                          MemorySegment rw, int n, MemorySegment status, int natMode) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) natSubmitMH.invokeExact(ENV.MEMORY, ctx, arena, arenaLen, desc, rw, n, status, natMode);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+        return ENV.returnLong();
+    }
+
     private static final MethodHandle setServiceMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
         "Java_io_vproxy_vpcsum_VPCsum_setService", long.class /* ctx */, int.class /* idleUs */);
 
     /** Low-latency flushes: batches of up to 512 packets from a registered arena go to a resident
      * GPU grid that polls a pinned mailbox, instead of a kernel launch each (about 13 us for 32
      * frames instead of 19).  The grid leaves after {@code idleUs} without a batch and restarts on
-     * the next submit; 0 turns it off.  Not critical: it may wait for batches in flight. */
+     * the next submit; 0 turns it off.  It waits for batches in flight. */
     public void setService(PNIEnv ENV, long ctx, int idleUs) throws java.io.IOException {
         ENV.reset();
         int ERR;

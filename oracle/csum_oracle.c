@@ -281,65 +281,101 @@ int orc_process_batch_mt(const uint8_t* arena, uint64_t arena_len, const vpcsum_
 }
 
 /* ---------------------------------------------------------------------------------------- */
-/* RFC 1624 vs Java: NAT / TTL rewrite restated as Java does it (setters + FULL recompute,  */
-/* SwitchUtils.applyNat SwitchUtils.java:522-542 -> getRawPacket(0)).                      */
+/* NAT / TTL rewrite restated as Java does it: setters, then a FULL recompute of the sums they */
+/* dirtied (SwitchUtils.applyNat SwitchUtils.java:522-542 -> getRawPacket(0)).               */
 /* ---------------------------------------------------------------------------------------- */
-void orc_nat4_java(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const vpcsum_nat4_t* rw,
-                   uint8_t* status) {
+void orc_nat_java(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const vpcsum_nat_t* rw,
+                  uint8_t* status) {
     uint64_t off = d->l3_off;
-    if (off > arena_len || (uint64_t)d->l3_len > arena_len - off || d->l3_ver != 4 ||
-        d->l3_len < 20 || d->l4_off < 20 || d->l4_off > d->l3_len || (d->l4_off & 3)) {
+    int ver = d->l3_ver, proto = d->l4_proto;
+    uint32_t len = d->l3_len, l4o = d->l4_off;
+    int ok = off <= arena_len && (uint64_t)len <= arena_len - off;
+    if (ok && ver == 4) ok = len >= 20 && l4o >= 20 && l4o <= len && !(l4o & 3);
+    else if (ok && ver == 6) ok = len >= 40 && l4o >= 40 && l4o <= len;
+    else ok = 0;
+    if (!ok) {
         if (status) *status = VPCSUM_S_BAD_DESC;
         return;
     }
     uint8_t* l3 = arena + off;
-    int l4 = (d->l4_proto == 6 || d->l4_proto == 17) &&
-             (uint32_t)(d->l3_len - d->l4_off) >= (uint32_t)orc_l4_field(d->l4_proto) + 2;
+    int fld = orc_l4_field((uint32_t)proto);
+    /* the L4 packet carries a checksum field (TcpPacket / UdpPacket / IcmpPacket) */
+    int l4sum = fld >= 0 && !(ver == 4 && proto == 58) && len - l4o >= (uint32_t)fld + 2;
+    /* pseudoHeaderChanges: IPv4 dirties TCP / UDP (Ipv4Packet.java:236-240), IPv6 also ICMP /
+     * ICMPv6 (Ipv6Packet.java:238-242) */
+    int addr_dirty = l4sum && (proto == 6 || proto == 17 || (ver == 6 && (proto == 1 || proto == 58)));
     int ip_dirty = 0, l4_dirty = 0;
-    if (rw->mask & VPCSUM_NAT_SRC) { memcpy(l3 + 12, rw->src, 4); ip_dirty = 1; l4_dirty = 1; } /* setSrc + pseudoHeaderChanges */
-    if (rw->mask & VPCSUM_NAT_DST) { memcpy(l3 + 16, rw->dst, 4); ip_dirty = 1; l4_dirty = 1; }
-    if (rw->mask & VPCSUM_NAT_DEC_TTL) { l3[8] = (uint8_t)(l3[8] - 1); ip_dirty = 1; }      /* setTtl(ttl-1) */
-    if (l4) {
-        if (rw->mask & VPCSUM_NAT_SPORT) { memcpy(l3 + d->l4_off, rw->sport, 2); l4_dirty = 1; }
-        if (rw->mask & VPCSUM_NAT_DPORT) { memcpy(l3 + d->l4_off + 2, rw->dport, 2); l4_dirty = 1; }
+    if (ver == 4) {
+        if (rw->mask & VPCSUM_NAT_SRC) { memcpy(l3 + 12, rw->src, 4); ip_dirty = 1; l4_dirty |= addr_dirty; } /* setSrc :433-445 */
+        if (rw->mask & VPCSUM_NAT_DST) { memcpy(l3 + 16, rw->dst, 4); ip_dirty = 1; l4_dirty |= addr_dirty; } /* setDst :447-458 */
+        if (rw->mask & VPCSUM_NAT_SET_TTL) { l3[8] = rw->ttl; ip_dirty = 1; }                     /* setTtl(ttl) :401-407 */
+        if (rw->mask & VPCSUM_NAT_DEC_TTL) { l3[8] = (uint8_t)(l3[8] - 1); ip_dirty = 1; }         /* setTtl(ttl-1) */
     } else {
-        l4_dirty = 0;
+        if (rw->mask & VPCSUM_NAT_SRC) { memcpy(l3 + 8, rw->src, 16); l4_dirty |= addr_dirty; }   /* setSrc :374-384 */
+        if (rw->mask & VPCSUM_NAT_DST) { memcpy(l3 + 24, rw->dst, 16); l4_dirty |= addr_dirty; }  /* setDst :386-396 */
+        if (rw->mask & VPCSUM_NAT_SET_TTL) l3[7] = rw->ttl;                    /* setHopLimit: nothing dirty */
+        if (rw->mask & VPCSUM_NAT_DEC_TTL) l3[7] = (uint8_t)(l3[7] - 1);
+    }
+    if (l4sum && (proto == 6 || proto == 17)) {   /* TcpPacket / UdpPacket.setSrcPort / setDstPort */
+        if (rw->mask & VPCSUM_NAT_SPORT) { memcpy(l3 + l4o, rw->sport, 2); l4_dirty = 1; }
+        if (rw->mask & VPCSUM_NAT_DPORT) { memcpy(l3 + l4o + 2, rw->dport, 2); l4_dirty = 1; }
     }
     if (ip_dirty) {
-        uint32_t c = orc_ipv4_header_csum(l3, d->l4_off);
+        uint32_t c = orc_ipv4_header_csum(l3, l4o);
         l3[10] = (uint8_t)(c >> 8); l3[11] = (uint8_t)c;
     }
     if (l4_dirty) {
         uint32_t c = 0;
-        orc_l4_csum(l3, d->l3_len, d->l4_off, 4, d->l4_proto, &c);
-        int fld = orc_l4_field(d->l4_proto);
-        l3[d->l4_off + fld] = (uint8_t)(c >> 8); l3[d->l4_off + fld + 1] = (uint8_t)c;
+        orc_l4_csum(l3, len, l4o, (uint32_t)ver, (uint32_t)proto, &c);
+        l3[l4o + fld] = (uint8_t)(c >> 8); l3[l4o + fld + 1] = (uint8_t)c;
     }
     if (status) *status = VPCSUM_S_DONE;
 }
 
-/* Batch of the above, split over threads (the CPU baseline of BASELINE config C5; frames of
- * one batch must not overlap). */
+/* The 16-B IPv4 entry: the same setters (rsv[0] = the SET_TTL value); IPv6 is rejected. */
+void orc_nat4_java(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const vpcsum_nat4_t* rw4,
+                   uint8_t* status) {
+    if (d->l3_ver != 4) {
+        if (status) *status = VPCSUM_S_BAD_DESC;
+        return;
+    }
+    vpcsum_nat_t rw;
+    memset(&rw, 0, sizeof(rw));
+    memcpy(rw.src, rw4->src, 4);
+    memcpy(rw.dst, rw4->dst, 4);
+    memcpy(rw.sport, rw4->sport, 2);
+    memcpy(rw.dport, rw4->dport, 2);
+    rw.mask = rw4->mask;
+    rw.ttl = rw4->rsv[0];
+    orc_nat_java(arena, arena_len, d, &rw, status);
+}
+
+/* Batches of the above, split over threads (the CPU baseline of BASELINE config C5; frames of
+ * one batch must not overlap).  fmt 0: vpcsum_nat4_t entries, 1: vpcsum_nat_t. */
 typedef struct {
-    uint8_t* arena; uint64_t arena_len; const vpcsum_desc_t* d; const vpcsum_nat4_t* rw;
+    uint8_t* arena; uint64_t arena_len; const vpcsum_desc_t* d; const void* rw; int fmt;
     uint8_t* status; uint32_t lo, hi;
 } orc_nat_job;
 
 static void* orc_nat_job_run(void* p) {
     orc_nat_job* j = (orc_nat_job*)p;
-    for (uint32_t i = j->lo; i < j->hi; ++i)
-        orc_nat4_java(j->arena, j->arena_len, j->d + i, j->rw + i, j->status ? j->status + i : NULL);
+    for (uint32_t i = j->lo; i < j->hi; ++i) {
+        if (j->fmt == 0)
+            orc_nat4_java(j->arena, j->arena_len, j->d + i, (const vpcsum_nat4_t*)j->rw + i, j->status ? j->status + i : NULL);
+        else
+            orc_nat_java(j->arena, j->arena_len, j->d + i, (const vpcsum_nat_t*)j->rw + i, j->status ? j->status + i : NULL);
+    }
     return NULL;
 }
 
-int orc_nat4_java_batch(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const vpcsum_nat4_t* rw,
-                        uint32_t n, uint8_t* status, int nthreads) {
+int orc_nat_java_batch(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const void* rw, int fmt,
+                       uint32_t n, uint8_t* status, int nthreads) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
     orc_nat_job jobs[256];
     for (int t = 0; t < nthreads; ++t) {
-        jobs[t].arena = arena; jobs[t].arena_len = arena_len; jobs[t].d = d; jobs[t].rw = rw;
+        jobs[t].arena = arena; jobs[t].arena_len = arena_len; jobs[t].d = d; jobs[t].rw = rw; jobs[t].fmt = fmt;
         jobs[t].status = status;
         jobs[t].lo = (uint32_t)((uint64_t)n * t / nthreads);
         jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
@@ -347,6 +383,11 @@ int orc_nat4_java_batch(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t*
     }
     for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
     return 0;
+}
+
+int orc_nat4_java_batch(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const vpcsum_nat4_t* rw,
+                        uint32_t n, uint8_t* status, int nthreads) {
+    return orc_nat_java_batch(arena, arena_len, d, rw, 0, n, status, nthreads);
 }
 
 /* ---------------------------------------------------------------------------------------- */

@@ -31,13 +31,15 @@ LIB_PATH = os.path.join(HERE, "build", "liborc.so")
 F_IP, F_L4, F_RAW, F_L4P = 0x01, 0x02, 0x04, 0x08
 S_IP_OK, S_L4_OK, S_UDP_NOCSUM, S_DONE, S_BAD_DESC = 0x01, 0x02, 0x04, 0x40, 0x80
 MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
-NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL = 0x01, 0x02, 0x04, 0x08, 0x10
+NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL, NAT_SET_TTL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 
 DESC_DTYPE = np.dtype([("l3_off", "<u8"), ("l3_len", "<u2"), ("l4_off", "<u2"), ("l3_ver", "u1"),
                        ("l4_proto", "u1"), ("flags", "u1"), ("rsv", "u1")])
 NAT4_DTYPE = np.dtype([("src", "u1", 4), ("dst", "u1", 4), ("sport", "u1", 2), ("dport", "u1", 2),
                        ("mask", "u1"), ("rsv", "u1", 3)])
-assert DESC_DTYPE.itemsize == 16 and NAT4_DTYPE.itemsize == 16
+NAT_DTYPE = np.dtype([("src", "u1", 16), ("dst", "u1", 16), ("sport", "u1", 2), ("dport", "u1", 2),
+                      ("mask", "u1"), ("ttl", "u1"), ("rsv", "u1", 10)])
+assert DESC_DTYPE.itemsize == 16 and NAT4_DTYPE.itemsize == 16 and NAT_DTYPE.itemsize == 48
 
 # Consts.java:24-31
 IP_PROTOCOL_ICMP, IP_PROTOCOL_TCP, IP_PROTOCOL_UDP, IP_PROTOCOL_ICMPv6 = 1, 6, 17, 58
@@ -381,6 +383,46 @@ def pure_process(l3: bytes, info: L3Info, flags: int) -> tuple[int, int]:
     return ipc, l4c
 
 
+def nat_java_pure(l3: bytearray, ver: int, proto: int, l3_len: int, l4_off: int, rw) -> None:
+    """NAT / TTL rewrite as Java does it, in place on one L3 packet: the setters
+    (Ipv4Packet.setSrc/setDst/setTtl, Ipv4Packet.java:401-407, 433-458; Ipv6Packet.setSrc/setDst/
+    setHopLimit, Ipv6Packet.java:354-396; TcpPacket/UdpPacket.setSrcPort/setDstPort) mark the sums
+    dirty (pseudoHeaderChanges: Ipv4Packet.java:236-240, Ipv6Packet.java:238-242) and
+    getRawPacket(0) recomputes them in full.  rw: one NAT_DTYPE record."""
+    m = int(rw["mask"])
+    fld = L4_FIELD.get(proto, -1)
+    l4sum = fld >= 0 and not (ver == 4 and proto == IP_PROTOCOL_ICMPv6) and l3_len - l4_off >= fld + 2
+    addr_dirty = l4sum and (proto in (IP_PROTOCOL_TCP, IP_PROTOCOL_UDP) or
+                            (ver == 6 and proto in (IP_PROTOCOL_ICMP, IP_PROTOCOL_ICMPv6)))
+    ip_dirty = l4_dirty = False
+    a = 12 if ver == 4 else 8
+    alen = 4 if ver == 4 else 16
+    if m & NAT_SRC:
+        l3[a:a + alen] = bytes(rw["src"][:alen])
+        ip_dirty, l4_dirty = ver == 4, l4_dirty or addr_dirty
+    if m & NAT_DST:
+        l3[a + alen:a + 2 * alen] = bytes(rw["dst"][:alen])
+        ip_dirty, l4_dirty = ver == 4, l4_dirty or addr_dirty
+    t = 8 if ver == 4 else 7
+    if m & NAT_SET_TTL:
+        l3[t] = int(rw["ttl"])
+        ip_dirty = ip_dirty or ver == 4
+    if m & NAT_DEC_TTL:
+        l3[t] = (l3[t] - 1) & 0xFF
+        ip_dirty = ip_dirty or ver == 4
+    if l4sum and proto in (IP_PROTOCOL_TCP, IP_PROTOCOL_UDP):
+        if m & NAT_SPORT:
+            l3[l4_off:l4_off + 2] = bytes(rw["sport"])
+            l4_dirty = True
+        if m & NAT_DPORT:
+            l3[l4_off + 2:l4_off + 4] = bytes(rw["dport"])
+            l4_dirty = True
+    if ip_dirty:
+        l3[10:12] = ipv4_header_csum(bytes(l3), l4_off).to_bytes(2, "big")
+    if l4_dirty:
+        l3[l4_off + fld:l4_off + fld + 2] = l4_csum(bytes(l3), l3_len, l4_off, ver, proto).to_bytes(2, "big")
+
+
 # ----------------------------------------------------------------------------------------
 # C oracle (same algorithm, for batches and the timed CPU baseline)
 # ----------------------------------------------------------------------------------------
@@ -408,6 +450,8 @@ class Oracle:
         L.orc_nat4_java.argtypes = [P, U64, P, P, P]
         L.orc_nat4_java_batch.argtypes = [P, U64, P, P, U32, P, ctypes.c_int]
         L.orc_nat4_java_batch.restype = ctypes.c_int
+        L.orc_nat_java_batch.argtypes = [P, U64, P, P, ctypes.c_int, U32, P, ctypes.c_int]
+        L.orc_nat_java_batch.restype = ctypes.c_int
         L.orc_rng.argtypes = [U64, U64, U64]
         L.orc_rng.restype = U64
         self.L = L
@@ -449,6 +493,17 @@ class Oracle:
         rw = np.ascontiguousarray(rw)
         rc = self.L.orc_nat4_java_batch(self._p(arena), arena.nbytes, self._p(desc), self._p(rw), len(desc),
                                         self._p(status), threads)
+        assert rc == 0
+        return status
+
+    def nat_java(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray, threads: int = 1):
+        """48-B vpcsum_nat_t entries (IPv4 and IPv6), Java semantics; in order on one thread."""
+        status = np.zeros(len(desc), np.uint8)
+        desc = np.ascontiguousarray(desc)
+        rw = np.ascontiguousarray(rw)
+        assert rw.dtype == NAT_DTYPE
+        rc = self.L.orc_nat_java_batch(self._p(arena), arena.nbytes, self._p(desc), self._p(rw), 1, len(desc),
+                                       self._p(status), threads)
         assert rc == 0
         return status
 

@@ -1,7 +1,8 @@
 // C-ABI consumer in plain C++ (no torch, no Python): what a JNI/Panama-side native or any other
 // host binds.  Builds the reference's udpIpv4Example / tcpIpv4SynExample frames
 // (TestPacket.java:459-494, 329-378), checksums them through vpcsum_ctx_* and through the PNI
-// entry points, and checks the values the reference test pins (0x7f41/0xdf0d, 0x87e4/0xf3ff).
+// entry points, and checks the values the reference test pins (0x7f41/0xdf0d, 0x87e4/0xf3ff);
+// then NAT-rewrites them through the PNI entry (zero-copy and staged) and verifies the result.
 // Build: g++ -std=c++17 -I include tests/cpp/capi_smoke.cpp -L vproxy_amd -lvpcsum -o capi_smoke
 #include <stdio.h>
 #include <stdlib.h>
@@ -84,6 +85,31 @@ int main() {
     CHECK(vpcsum_ctx_stats((vpcsum_ctx_t*)(intptr_t)h, &sb, nullptr) == 0 && sb == 3, "service batches %llu", (unsigned long long)sb);
     CHECK(Java_io_vproxy_vpcsum_VPCsum_setService(&envv, h, -1) == -1, "negative idle must throw");
     CHECK(Java_io_vproxy_vpcsum_VPCsum_setService(&envv, h, 0) == 0, "pni service off");
+    // NAT through the PNI entry (SwitchUtils.applyNat for a batch): setSrcPort(121) + setDst on
+    // both frames, zero-copy on the registered arena and staged from a pageable copy; the frames
+    // must verify afterwards (sums updated as Java's recompute leaves them)
+    vpcsum_nat_t rw[2];
+    memset(rw, 0, sizeof(rw));
+    for (int i = 0; i < 2; ++i) {
+        rw[i].sport[1] = 121;
+        rw[i].dst[0] = 1; rw[i].dst[1] = 2; rw[i].dst[2] = 3; rw[i].dst[3] = 4;
+        rw[i].mask = VPCSUM_NAT_SPORT | VPCSUM_NAT_DST;
+    }
+    std::vector<uint8_t> copy(arena);
+    for (int mode = 0; mode < 2; ++mode) {
+        for (int staged = 0; staged < 2; ++staged) {
+            uint8_t* a = staged ? copy.data() : arena.data();
+            memset(&envl, 0, sizeof(envl));
+            CHECK(Java_io_vproxy_vpcsum_VPCsum_natSubmit(&envl, h, a, (int64_t)arena.size(), d, rw, 2, st, mode) == 0, "pni natSubmit");
+            CHECK(Java_io_vproxy_vpcsum_VPCsum_waitFor(&envv, h, envl.return_) == 0, "nat wait");
+            CHECK(st[0] == VPCSUM_S_DONE && st[1] == VPCSUM_S_DONE, "nat status %02x %02x", st[0], st[1]);
+            CHECK(a[14 + 20 + 1] == 121 && a[2048 + 14 + 20 + 1] == 121 && a[14 + 16] == 1, "nat bytes");
+            memset(&envl, 0, sizeof(envl));
+            CHECK(Java_io_vproxy_vpcsum_VPCsum_submit(&envl, h, a, (int64_t)arena.size(), d, 2, out, st, VPCSUM_MODE_VERIFY) == 0, "verify");
+            CHECK(Java_io_vproxy_vpcsum_VPCsum_waitFor(&envv, h, envl.return_) == 0, "verify wait");
+            CHECK(st[0] == (VPCSUM_S_DONE | VPCSUM_S_IP_OK | VPCSUM_S_L4_OK) && st[1] == st[0], "after nat %02x %02x", st[0], st[1]);
+        }
+    }
     memset(&envl, 0, sizeof(envl));
     CHECK(Java_io_vproxy_vpcsum_VPCsum_create(&envl, 0, -1, 64) == -1, "pni bad args");
     CHECK(envl.ex.type && strcmp(envl.ex.type, "java.lang.IllegalArgumentException") == 0, "ex type");

@@ -6,8 +6,10 @@ Outputs (committed, data only):
                    values that test pins (asserted or embedded in the frames it round-trips).
   pcap/*.pcap   -- the reference's pcap fixtures (test/src/test/resources/pcap/, MIT), copied
                    byte for byte as data.
-  nat.json      -- checkPartialAndModify-style rewrites of the KAT frames (TestPacket.java:137-181)
-                   with the expected bytes produced by the oracle's Java-semantics full recompute.
+  nat.json      -- the reference's own checkPartialAndModify rewrites of the KAT frames
+                   (TestPacket.java:137-181, the setSrc / setDst / setTtl / setHopLimit /
+                   setSrcPort / setDstPort calls of each KAT test) and IPInputRoute's TTL decrement,
+                   with the expected bytes of the oracle's Java-semantics full recompute.
 
 Usage:  python tests/golden/make_golden.py [/root/reference]
 """
@@ -112,40 +114,79 @@ def main(ref: str) -> None:
         if fn.endswith(".pcap"):
             shutil.copyfile(os.path.join(ref, PCAP_DIR, fn), os.path.join(HERE, "pcap", fn))
 
-    # NAT rewrites mirroring checkPartialAndModify (TestPacket.java:137-181): expected bytes from
-    # the oracle's Java-semantics rewrite + full recompute.
+    # NAT rewrites: the reference's own checkPartialAndModify calls (TestPacket.java:137-181 and
+    # the lines below), parsed from the test source, plus the TTL decrement of IPInputRoute
+    # (core/.../vswitch/node/IPInputRoute.java:79-91).  Expected bytes: the oracle's
+    # Java-semantics rewrite + full recompute (oracle/csum_oracle.c:orc_nat_java).
+    import ipaddress
     from oracle import oracle as O
     import numpy as np
+    lines = src.split("\n")
+    calls = []
+    for ln, text in enumerate(lines, 1):
+        if "checkPartialAndModify(" in text and "void checkPartialAndModify" not in text:
+            call = text + (lines[ln] if text.rstrip().endswith(",") else "")
+            calls.append((ln, call))
+    methods = {k["name"]: method_body(src, k["name"])[1:] for k in kats}
+
+    def rewrite_of(call: str):
+        m = re.search(r"set(Src|Dst)\(\(IPv[46]\) IP\.from\(\"([^\"]+)\"\)\)", call)
+        if m:
+            return ("NAT_" + m.group(1).upper(), ipaddress.ip_address(m.group(2)).packed)
+        m = re.search(r"\.(setTtl|setHopLimit)\((\d+)\)", call)
+        if m:
+            return ("NAT_SET_TTL", int(m.group(2)))
+        m = re.search(r"\.set(Src|Dst)Port\((\d+)\)", call)
+        if m:
+            return ("NAT_" + m.group(1).upper()[0] + "PORT", int(m.group(2)))
+        return None
+
+    def entry(kind, val):
+        rw = np.zeros(1, O.NAT_DTYPE)
+        if kind in ("NAT_SRC", "NAT_DST"):
+            rw[0][kind[4:].lower()][:len(val)] = list(val)
+        elif kind == "NAT_SET_TTL":
+            rw[0]["ttl"] = val
+        elif kind in ("NAT_SPORT", "NAT_DPORT"):
+            rw[0][kind[4:].lower()] = [val >> 8, val & 0xFF]
+        rw[0]["mask"] = getattr(O, kind)
+        return rw
+
     nat_cases = []
-    rewrites = [("setSrc", O.NAT_SRC), ("setDst", O.NAT_DST), ("setSrcPort", O.NAT_SPORT),
-                ("setDstPort", O.NAT_DPORT), ("setTtl", O.NAT_DEC_TTL)]
     orc = O.Oracle()
     for k in kats:
-        if k["ver"] != 4 or k["proto"] not in (6, 17, 1):
-            continue
+        a, b = methods[k["name"]]
+        mine = [(ln, c) for ln, c in calls if a <= ln <= b]
+        label = {"NAT_SRC": "setSrc({})", "NAT_DST": "setDst({})", "NAT_SET_TTL": "setTtl / setHopLimit({})",
+                 "NAT_SPORT": "setSrcPort({})", "NAT_DPORT": "setDstPort({})"}
+        todo = []
+        for ln, c in mine:
+            r = rewrite_of(c)
+            if r is not None:
+                v = str(ipaddress.ip_address(r[1])) if r[0] in ("NAT_SRC", "NAT_DST") else r[1]
+                todo.append((f"{TESTPACKET}:{ln}", label[r[0]].format(v), r))
+        if k["ver"] == 4 and k["proto"] in (1, 6, 17):
+            todo.append(("core/src/main/java/io/vproxy/vswitch/node/IPInputRoute.java:79-91",
+                         "TTL decrement (setTtl(ttl - 1))", ("NAT_DEC_TTL", None)))
         fr = bytes.fromhex(k["hex"])
         l3off = 0 if k["layer"] == "l3" else 14
         info, err = O.parse_l3(fr, l3off, len(fr) - l3off)
         assert err is None
-        for rname, mask in rewrites:
-            if k["proto"] == 1 and mask in (O.NAT_SPORT, O.NAT_DPORT):
-                continue
+        for srcline, text, (kind, val) in todo:
             arena = np.frombuffer(fr, np.uint8).copy()
             desc = np.zeros(1, O.DESC_DTYPE)
-            desc[0] = (info.l3_off, info.l3_len, info.l4_off, 4, info.proto, O.desc_flags_for(info), 0)
-            rw = np.zeros(1, O.NAT4_DTYPE)
-            rw[0]["src"] = [1, 2, 3, 4]
-            rw[0]["dst"] = [1, 2, 3, 4]
-            rw[0]["sport"] = [0, 121]
-            rw[0]["dport"] = [0, 121]
-            rw[0]["mask"] = mask
-            orc.nat4_java(arena, desc, rw)
-            nat_cases.append(dict(kat=k["name"], rewrite=rname, mask=mask, l3_off=l3off,
-                                  before=fr.hex(), after=arena.tobytes().hex()))
+            desc[0] = (info.l3_off, info.l3_len, info.l4_off, info.ver, info.proto, O.desc_flags_for(info), 0)
+            rw = entry(kind, val)
+            st = orc.nat_java(arena, desc, rw)
+            assert st[0] == O.S_DONE
+            nat_cases.append(dict(kat=k["name"], ver=info.ver, rewrite=text, source=srcline, mask=int(rw[0]["mask"]),
+                                  entry=rw.tobytes().hex(), l3_off=l3off, before=fr.hex(),
+                                  after=arena.tobytes().hex()))
+    assert sum(c["source"].startswith(TESTPACKET) for c in nat_cases) == 18   # 3 + 3 + 4 x 3
     with open(os.path.join(HERE, "nat.json"), "w") as f:
-        json.dump({"generator": "tests/golden/make_golden.py (oracle full recompute)",
-                   "rewrite": {"src": "1.2.3.4", "dst": "1.2.3.4", "sport": 121, "dport": 121,
-                               "ttl": "decrement (setTtl(ttl-1), IPInputRoute.java:79-91)"},
+        json.dump({"generator": "tests/golden/make_golden.py (rewrites parsed from TestPacket.java; expected "
+                                "bytes from the oracle's Java-semantics full recompute)",
+                   "entry": "vpcsum_nat_t (48 B, include/vpcsum.h), hex",
                    "cases": nat_cases}, f, indent=1)
     print(f"kats={len(kats)} nat={len(nat_cases)}")
 

@@ -235,7 +235,8 @@ def _nat_batch(orc, n, seed=3, corrupt=0.0, udp_zero=0.0, pad=0, workload=O.SYNT
     rw["dst"] = rng.integers(0, 256, (n, 4))
     rw["sport"] = rng.integers(0, 256, (n, 2))
     rw["dport"] = rng.integers(0, 256, (n, 2))
-    rw["mask"] = rng.integers(0, 32, n)
+    rw["mask"] = rng.integers(0, 64, n)
+    rw["rsv"][:, 0] = rng.integers(0, 256, n)     # the VPCSUM_NAT_SET_TTL value
     for i in range(n):
         l3 = int(desc[i]["l3_off"])
         if rng.random() < corrupt:
@@ -297,22 +298,132 @@ def test_nat_strict_java_on_invalid_input(V, orc):
     assert not np.array_equal(got_fast, want)
 
 
+def _gpu_nat48(V, arena_np, desc, rw, mode):
+    import torch
+    arena = dev(arena_np.copy())
+    st = torch.zeros(len(desc), dtype=torch.uint8, device="cuda")
+    V.nat(arena, V.desc_to_tensor(desc), dev(rw.view(np.uint8)), len(desc), st, mode)
+    torch.cuda.synchronize()
+    return arena.cpu().numpy(), st.cpu().numpy()
+
+
+def _nat4_of(rw48):
+    """The 16-B IPv4 entries of 48-B ones (rsv[0] = the SET_TTL value)."""
+    r4 = np.zeros(len(rw48), O.NAT4_DTYPE)
+    r4["src"] = rw48["src"][:, :4]
+    r4["dst"] = rw48["dst"][:, :4]
+    r4["sport"] = rw48["sport"]
+    r4["dport"] = rw48["dport"]
+    r4["mask"] = rw48["mask"]
+    r4["rsv"][:, 0] = rw48["ttl"]
+    return r4
+
+
 def test_nat_golden(V):
+    """The reference's own checkPartialAndModify rewrites (setSrc / setDst 1.2.3.4 and ::2,
+    setTtl(5), setHopLimit(5), setSrcPort / setDstPort(121)) and IPInputRoute's TTL decrement on
+    the TestPacket frames: both entry formats, both kernels, RFC 1624 and strict Java."""
     d = json.load(open(os.path.join(GOLD, "nat.json")))
-    for mode in (0, 1):
-        for c in d["cases"]:
-            fr = bytes.fromhex(c["before"])
-            info, _ = O.parse_l3(fr, c["l3_off"], len(fr) - c["l3_off"])
-            desc = np.array([(info.l3_off, info.l3_len, info.l4_off, 4, info.proto, O.desc_flags_for(info), 0)],
-                            dtype=O.DESC_DTYPE)
-            rw = np.zeros(1, O.NAT4_DTYPE)
-            rw[0]["src"] = [1, 2, 3, 4]
-            rw[0]["dst"] = [1, 2, 3, 4]
-            rw[0]["sport"] = [0, 121]
-            rw[0]["dport"] = [0, 121]
-            rw[0]["mask"] = c["mask"]
-            got, _ = _gpu_nat(V, np.frombuffer(fr, np.uint8), desc, rw, mode)
+    assert {c["ver"] for c in d["cases"]} == {4, 6}
+    for c in d["cases"]:
+        fr = bytes.fromhex(c["before"])
+        info, _ = O.parse_l3(fr, c["l3_off"], len(fr) - c["l3_off"])
+        desc = np.array([(info.l3_off, info.l3_len, info.l4_off, info.ver, info.proto, O.desc_flags_for(info), 0)],
+                        dtype=O.DESC_DTYPE)
+        rw = np.frombuffer(bytes.fromhex(c["entry"]), O.NAT_DTYPE).copy()
+        a = np.frombuffer(fr, np.uint8)
+        for mode in (V.NAT_RFC1624, V.NAT_STRICT_JAVA, V.NAT_RFC1624 | 0x100, V.NAT_STRICT_JAVA | 0x100):
+            got, st = _gpu_nat48(V, a, desc, rw, mode)
             assert got.tobytes().hex() == c["after"], (c["kat"], c["rewrite"], mode)
+            assert st[0] == O.S_DONE
+            got, st = _gpu_nat(V, a, desc, _nat4_of(rw), mode)
+            if info.ver == 4:
+                assert got.tobytes().hex() == c["after"], (c["kat"], c["rewrite"], mode, "nat4")
+            else:   # the 16-B entry carries IPv4 addresses only: IPv6 is refused, untouched
+                assert st[0] == O.S_BAD_DESC and got.tobytes() == fr
+
+
+def _nat48_batch(orc, rng, n, pad=0, corrupt=0.0):
+    """FUZZ packets (IPv4 with options, IPv6, TCP / UDP / ICMP / ICMPv6) with valid sums, 10% UDP
+    stored 0, and random 48-B rewrites with every mask bit."""
+    arena, desc = orc.synth(n, 9088, pad, O.SYNTH_FUZZ, O.SEED, int(rng.integers(0, 1 << 30)))
+    orc.process(arena, desc, O.MODE_COMPUTE, write=True)
+    for d in desc:
+        o, l4 = int(d["l3_off"]), int(d["l4_off"])
+        if d["l4_proto"] == 17 and rng.random() < 0.1:
+            arena[o + l4 + 6:o + l4 + 8] = 0
+        if rng.random() < corrupt:
+            arena[o + l4 + 1 + (int(d["l3_len"]) - l4) // 2] ^= 0x5A   # invalid L4 sums
+    rw = np.zeros(n, O.NAT_DTYPE)
+    rw.view(np.uint8).reshape(n, 48)[:, :38] = rng.integers(0, 256, (n, 38), dtype=np.uint8)
+    rw["mask"] = rng.integers(0, 64, n)
+    return arena, desc, rw
+
+
+@pytest.mark.parametrize("pad", [0, 1, 2, 14])
+def test_nat_v4_v6_against_java(V, orc, pad):
+    """vpcsum_nat_async on IPv4 and IPv6: RFC 1624 equals Java's full recompute on valid input,
+    strict Java equals it on any input; the wide kernel and the byte-access kernel agree."""
+    rng = np.random.default_rng(100 + pad)
+    arena, desc, rw = _nat48_batch(orc, rng, 1500, pad)
+    want = arena.copy()
+    orc.nat_java(want, desc, rw)
+    for mode in (V.NAT_RFC1624, V.NAT_STRICT_JAVA, V.NAT_RFC1624 | 0x100, V.NAT_STRICT_JAVA | 0x100,
+                 V.NAT_RFC1624 | 0x1000, V.NAT_RFC1624 | 0x3000):
+        got, st = _gpu_nat48(V, arena, desc, rw, mode)
+        assert np.all(st == O.S_DONE), hex(mode)
+        assert np.array_equal(got, want), hex(mode)
+    # corrupted inputs: strict Java still matches, RFC 1624 diverges exactly there
+    arena, desc, rw = _nat48_batch(orc, rng, 800, pad, corrupt=0.3)
+    want = arena.copy()
+    orc.nat_java(want, desc, rw)
+    got, _ = _gpu_nat48(V, arena, desc, rw, V.NAT_STRICT_JAVA)
+    assert np.array_equal(got, want)
+    got, _ = _gpu_nat48(V, arena, desc, rw, V.NAT_RFC1624)
+    assert not np.array_equal(got, want)
+
+
+def test_nat_edge_packets_v6(V, orc):
+    """The crafted edge packets (IPv6 extension headers with odd l4_off, ICMPv4 in IPv6, sums of
+    0, UDP stored 0) under 48-B rewrites: wide window where it fits, byte access beyond it."""
+    import edgevec as E
+    pk = [p for p in E.edge_packets(np.random.default_rng(7)) if p["l3_len"] <= 9000]
+    for pad in (0, 3):
+        arena, desc = E.pack(pk, pad)
+        rng = np.random.default_rng(pad)
+        rw = np.zeros(len(desc), O.NAT_DTYPE)
+        rw.view(np.uint8).reshape(-1, 48)[:, :38] = rng.integers(0, 256, (len(desc), 38), dtype=np.uint8)
+        rw["mask"] = rng.integers(1, 64, len(desc))
+        want = arena.copy()
+        orc.nat_java(want, desc, rw)
+        for mode in (V.NAT_RFC1624, V.NAT_STRICT_JAVA):
+            got, st = _gpu_nat48(V, arena, desc, rw, mode)
+            assert np.array_equal(got, want), (pad, mode)
+
+
+@pytest.mark.parametrize("registered", [False, True])
+def test_ctx_nat_submit(V, orc, registered):
+    """vpcsum_ctx_nat_submit on host frames: staged (pageable arena: headers copied back at wait)
+    and zero-copy (registered arena: rewritten in place), both modes, rejected descriptors
+    untouched."""
+    rng = np.random.default_rng(5 + registered)
+    arena, desc, rw = _nat48_batch(orc, rng, 700, 14)
+    desc = desc.copy()
+    desc["l3_ver"][::50] = 5                 # rejected
+    arena = np.concatenate([arena, np.zeros(4096, np.uint8)])
+    ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=len(desc))
+    if registered:
+        ctx.register(arena)
+    base = arena.copy()
+    for mode in (V.NAT_RFC1624, V.NAT_STRICT_JAVA):
+        a = arena if registered else base.copy()
+        a[:] = base
+        want = base.copy()
+        wst = orc.nat_java(want, desc, rw)
+        st = ctx.nat(a, desc, rw, mode)
+        assert np.array_equal(st, wst), mode
+        assert np.array_equal(a, want), mode
+    ctx.close()
 
 
 def test_parse_ether_matches_reference_rules(V):
@@ -401,6 +512,12 @@ def test_context_pipeline(V, orc):
     ctx.register(out)
     ctx.pipeline(arena, stride, 1504, desc, out, chunks=8)
     assert np.array_equal(out, want)
+    # MODE_WRITE: the checksum fields land in the host frames too
+    want_arena = arena.copy()
+    orc.process(want_arena, desc, O.MODE_COMPUTE, write=True)
+    out[:] = 0
+    ctx.pipeline(arena, stride, 1504, desc, out, mode=O.MODE_WRITE, chunks=8)
+    assert np.array_equal(out, want) and np.array_equal(arena, want_arena)
     # a descriptor outside the copied part of its chunk's frames is refused, not read
     d2 = desc.copy()
     ctx.register(d2)   # registered until close: keep the array alive
@@ -953,3 +1070,23 @@ def test_unregister_with_batch_in_flight(V, orc, service):
     out2, _ = ctx.run(arena, d)
     assert np.array_equal(out2, want)
     ctx.close()
+
+
+def test_egress_small_flush_hand_back(V, orc):
+    """GpuCsumBatch's SMALL_FLUSH rule in the mirror: a flush below the threshold goes back to the
+    native path untouched (no GPU submit); from the threshold on it is computed on the GPU."""
+    from vproxy_amd import vswitch as S
+    n, stride = 12, 2048
+    arena, desc = orc.synth(n, stride, 14, O.SYNTH_C3, O.SEED, 321)
+    before = arena.copy()
+    want = arena.copy()
+    orc.process(want, desc[4:], O.MODE_COMPUTE, write=True)
+    batch = S.EgressBatch(arena, capacity=64, small_flush=5)
+    for d in desc[:4]:
+        batch.defer(int(d["l3_off"]), int(d["l3_len"]), int(d["l4_off"]), 4, int(d["l4_proto"]), int(d["flags"]))
+    assert batch.complete_tx() == 0 and np.array_equal(arena, before)
+    assert len(batch.handed_back) == 1 and len(batch.handed_back[0]) == 4
+    for d in desc[4:]:
+        batch.defer(int(d["l3_off"]), int(d["l3_len"]), int(d["l4_off"]), 4, int(d["l4_proto"]), int(d["flags"]))
+    assert batch.complete_tx() == 8 and np.array_equal(arena, want)
+    batch.close()

@@ -78,3 +78,15 @@ def test_cpp_consumer_builds(libpath, tmp_path):
                            os.path.join(REPO, "tests", "cpp", "capi_smoke.cpp"), "-L", os.path.dirname(libpath),
                            "-lvpcsum", "-o", str(exe)])
     assert exe.exists()
+
+
+def test_pni_env_layout_and_errno(libpath, tmp_path):
+    """PNIEnv offsets equal the PNI runtime's (pni.h:15-73: message at 8, errno_ at 4104, return_
+    at 4112, 4128 bytes), checked by _Static_assert in a C file; running it throws through two PNI
+    entry points (argument errors, no GPU needed) and finds type, message and errno_ set."""
+    exe = tmp_path / "pni_layout"
+    subprocess.check_call(["gcc", "-std=c11", "-O1", "-Wall", "-I", os.path.join(REPO, "include"),
+                           os.path.join(REPO, "tests", "cpp", "pni_layout.c"), "-L", os.path.dirname(libpath),
+                           "-lvpcsum", "-Wl,-rpath," + os.path.dirname(libpath), "-o", str(exe)])
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "pni layout ok" in r.stdout, (r.returncode, r.stdout, r.stderr)

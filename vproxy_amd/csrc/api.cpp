@@ -7,6 +7,7 @@
 // Errors: plain functions return <0 and set a thread-local message; PNI functions store the
 // exception in env->ex exactly as the PNI runtime expects (base/src/main/c-generated/pni.h:74-82).
 #include <hip/hip_runtime.h>
+#include <errno.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -901,7 +902,7 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint
     if (!c || !h_arena || !h_desc || !h_out) return fail("vpcsum_ctx_pipeline: NULL argument");
     if (chunks == 0) chunks = 1;
     if (copy_bytes > stride) return fail("vpcsum_ctx_pipeline: copy_bytes > stride");
-    if (mode & ~VPCSUM_MODE_VERIFY) return fail("vpcsum_ctx_pipeline: bad mode");
+    if (mode & ~(VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_ctx_pipeline: bad mode");
     std::lock_guard<std::mutex> lk(c->mu);
     VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
     for (auto& s : c->slots)
@@ -911,6 +912,14 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint
         return fail("vpcsum_ctx_pipeline: chunk of %u frames exceeds context capacity", per);
     const bool pinned = is_registered(c, h_arena, (uint64_t)n * stride);
     if (!pinned) return fail("vpcsum_ctx_pipeline: host arena must be registered (vpcsum_ctx_register_arena)");
+    // MODE_WRITE: the kernels read the device copy and store the checksum fields straight into the
+    // host frames through the registered arena's mapping (2-B posted PCIe writes), so the frames
+    // need no copy back
+    uint8_t* w = nullptr;
+    if (mode & VPCSUM_MODE_WRITE) {
+        w = mapped_dev(c, h_arena, (uint64_t)n * stride);
+        if (!w) return fail("vpcsum_ctx_pipeline: MODE_WRITE needs the arena registered with this context");
+    }
     const bool desc_pinned = is_registered(c, (const uint8_t*)h_desc, (uint64_t)n * sizeof(vpcsum_desc_t));
     const bool out_pinned = is_registered(c, (const uint8_t*)h_out, (uint64_t)n * 4);
     if (!desc_pinned || !out_pinned) return fail("vpcsum_ctx_pipeline: descriptors and out must be registered");
@@ -938,7 +947,7 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint
                                    hipMemcpyHostToDevice, s.stream),
                   "pipeline H2D frames");
         VPC_CHECK(launch_csum(s.d_arena - (uint64_t)i0 * stride, (uint64_t)(i0 + m) * stride, s.d_desc, m, s.d_out,
-                              nullptr, nullptr, mode, nullptr, 0, 0, s.stream),
+                              nullptr, nullptr, mode & VPCSUM_MODE_VERIFY, w, 0, 0, s.stream),
                   "pipeline launch");
         VPC_CHECK(hipMemcpyAsync(h_out + i0, s.d_out, (size_t)m * 4, hipMemcpyDeviceToHost, s.stream), "pipeline D2H");
     }
@@ -949,11 +958,15 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint
 // ------------------------------------------------------------------------------------------
 // PNI entry points
 // ------------------------------------------------------------------------------------------
+// The exception travels in env->ex as PNIThrowException stores it (pni.h:74-80); errno_ carries
+// EINVAL for argument errors and EIO for failures of the device runtime (PNIStoreErrno's slot,
+// pni.h:86-89), so Java code that inspects it sees a meaningful value.
 static int pni_throw(void* env, const char* type) {
     PNIException_vpcsum* ex = (PNIException_vpcsum*)env;
     ex->type = (char*)type;
     strncpy(ex->message, g_err.c_str(), sizeof(ex->message));
     ex->message[sizeof(ex->message) - 1] = '\0';
+    ex->errno_ = strcmp(type, "java.lang.IllegalArgumentException") == 0 ? EINVAL : EIO;
     return -1;
 }
 

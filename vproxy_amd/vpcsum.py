@@ -19,7 +19,7 @@ from .build import LIB
 F_IP, F_L4, F_RAW, F_L4P = 0x01, 0x02, 0x04, 0x08
 S_IP_OK, S_L4_OK, S_UDP_NOCSUM, S_DONE, S_BAD_DESC = 0x01, 0x02, 0x04, 0x40, 0x80
 MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
-NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL = 0x01, 0x02, 0x04, 0x08, 0x10
+NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL, NAT_SET_TTL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 NAT_RFC1624, NAT_STRICT_JAVA = 0x00, 0x01
 SYNTH_C1, SYNTH_C2, SYNTH_C3, SYNTH_C4, SYNTH_FUZZ, SYNTH_C5 = 1, 2, 3, 4, 5, 6
 
@@ -27,16 +27,19 @@ DESC_DTYPE = np.dtype([("l3_off", "<u8"), ("l3_len", "<u2"), ("l4_off", "<u2"), 
                        ("l4_proto", "u1"), ("flags", "u1"), ("rsv", "u1")])
 NAT4_DTYPE = np.dtype([("src", "u1", 4), ("dst", "u1", 4), ("sport", "u1", 2), ("dport", "u1", 2),
                        ("mask", "u1"), ("rsv", "u1", 3)])
+NAT_DTYPE = np.dtype([("src", "u1", 16), ("dst", "u1", 16), ("sport", "u1", 2), ("dport", "u1", 2),
+                      ("mask", "u1"), ("ttl", "u1"), ("rsv", "u1", 10)])
 
 # Every symbol include/vpcsum.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "vpcsum_abi_version", "vpcsum_last_error", "vpcsum_device_count", "vpcsum_set_device",
-    "vpcsum_compute_async", "vpcsum_nat4_async", "vpcsum_parse_ether_async", "vpcsum_read_probe_async",
+    "vpcsum_compute_async", "vpcsum_nat4_async", "vpcsum_nat_async", "vpcsum_parse_ether_async", "vpcsum_read_probe_async",
     "vpcsum_pattern_probe_async",
     "vpcsum_synth_async", "vpcsum_event_create", "vpcsum_event_destroy", "vpcsum_event_record",
     "vpcsum_event_elapsed_ms", "vpcsum_stream_sync", "vpcsum_ctx_create", "vpcsum_ctx_destroy",
     "vpcsum_ctx_register_arena", "vpcsum_ctx_unregister_arena", "vpcsum_ctx_submit", "vpcsum_ctx_wait",
     "vpcsum_ctx_pipeline", "vpcsum_ctx_set_service", "vpcsum_ctx_stats", "vpcsum_ctx_verify_frames",
+    "vpcsum_ctx_nat_submit", "Java_io_vproxy_vpcsum_VPCsum_natSubmit",
     "Java_io_vproxy_vpcsum_VPCsum_create", "Java_io_vproxy_vpcsum_VPCsum_registerArena",
     "Java_io_vproxy_vpcsum_VPCsum_submit", "Java_io_vproxy_vpcsum_VPCsum_waitFor",
     "Java_io_vproxy_vpcsum_VPCsum_close", "Java_io_vproxy_vpcsum_VPCsum_setService",
@@ -65,6 +68,8 @@ def _declare(L):
         "vpcsum_set_device": ([I], I),
         "vpcsum_compute_async": ([P, U64, P, U32, P, P, U32, P], I),
         "vpcsum_nat4_async": ([P, U64, P, P, U32, P, U32, P], I),
+        "vpcsum_nat_async": ([P, U64, P, P, U32, P, U32, P], I),
+        "vpcsum_ctx_nat_submit": ([P, P, U64, P, P, U32, P, U32, P], I),
         "vpcsum_parse_ether_async": ([P, U64, P, P, U32, U8, P, P, P], I),
         "vpcsum_read_probe_async": ([P, U64, P, U32, P], I),
         "vpcsum_pattern_probe_async": ([P, U64, P, U32, P, U32, P], I),
@@ -155,6 +160,12 @@ def compute(arena, desc, n: int | None = None, out=None, status=None, mode: int 
 def nat4(arena, desc, rw, n: int, status=None, nat_mode: int = NAT_RFC1624, stream=None):
     _check(lib().vpcsum_nat4_async(_ptr(arena), arena.numel(), _ptr(desc), _ptr(rw), n, _ptr(status), nat_mode,
                                    _stream(stream)), "vpcsum_nat4_async")
+
+
+def nat(arena, desc, rw, n: int, status=None, nat_mode: int = NAT_RFC1624, stream=None):
+    """NAT / TTL rewrite with 48-B vpcsum_nat_t entries (IPv4 and IPv6): `rw` a uint8 tensor of n x 48."""
+    _check(lib().vpcsum_nat_async(_ptr(arena), arena.numel(), _ptr(desc), _ptr(rw), n, _ptr(status), nat_mode,
+                                  _stream(stream)), "vpcsum_nat_async")
 
 
 def parse_ether(arena, frame_off, frame_len, n: int, desc, status=None, flags: int = F_IP | F_L4, stream=None):
@@ -251,6 +262,22 @@ class Context:
                "vpcsum_ctx_verify_frames")
         self.wait(t.value)
         return out, status
+
+    def nat_submit(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray, status: np.ndarray | None = None,
+                   nat_mode: int = NAT_RFC1624) -> int:
+        """NAT / TTL rewrites of host frames (vpcsum_ctx_nat_submit); rw: NAT_DTYPE entries."""
+        assert rw.dtype == NAT_DTYPE and len(rw) >= len(desc)
+        t = ctypes.c_uint64()
+        _check(lib().vpcsum_ctx_nat_submit(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data,
+                                           rw.ctypes.data, len(desc), None if status is None else status.ctypes.data,
+                                           nat_mode, ctypes.byref(t)), "vpcsum_ctx_nat_submit")
+        self._inflight[t.value & 1] = (arena, desc, rw, status)
+        return t.value
+
+    def nat(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray, nat_mode: int = NAT_RFC1624) -> np.ndarray:
+        status = np.zeros(len(desc), np.uint8)
+        self.wait(self.nat_submit(arena, desc, rw, status, nat_mode))
+        return status
 
     def set_service(self, idle_us: int):
         """Low-latency flushes from registered arenas (persistent service grid); 0 = off."""

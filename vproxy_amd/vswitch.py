@@ -44,9 +44,13 @@ class EgressBatch:
     (vpcsum_ctx_set_service) instead of a kernel launch each."""
 
     def __init__(self, arena: np.ndarray, capacity: int = 4096, device: int = 0, register: bool = True,
-                 service_idle_us: int = 0):
+                 service_idle_us: int = 0, small_flush: int = 0):
         self.arena = arena
         self.capacity = capacity
+        # flushes of fewer frames are handed back to the caller's native path (GpuCsumBatch.flush,
+        # SMALL_FLUSH: the GPU breaks even at ~5 frames per flush)
+        self.small_flush = small_flush
+        self.handed_back: list[np.ndarray] = []
         self.ctx = V.Context(device, max_arena=max(arena.nbytes, 1 << 16), max_pkts=capacity)
         if register:
             self.ctx.register(arena)
@@ -75,6 +79,11 @@ class EgressBatch:
         if self.n == 0:
             return 0
         n = self.n
+        if n < self.small_flush:
+            self.handed_back.append(self.desc[:n].copy())
+            self.stats["handed_back"] = self.stats.get("handed_back", 0) + n
+            self.n = 0
+            return 0
         t = self.ctx.submit(self.arena, self.desc[:n], self.out[:n], self.status[:n], V.MODE_WRITE)
         self.ctx.wait(t)
         bad = int(np.count_nonzero(self.status[:n] & V.S_BAD_DESC))
