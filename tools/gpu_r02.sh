@@ -1,0 +1,45 @@
+#!/bin/bash
+# Round-2 measurement call: bench lines of every config, kernel trace of the headline, PMC passes
+# (C2, C1, C3, NAT full and read-only), host path.  Every GPU step has its own time limit; a
+# crash / abort / timeout (exit > 1) ends the script.  usage: tools/gpu_r02.sh <tag> [parts]
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${1:-r02}; PARTS=${2:-bench,trace,pmc,host}
+step() {  # name, limit, cmd...
+  local name=$1 lim=$2; shift 2
+  echo "=== $name $(date +%T)"
+  timeout -k 10 "$lim" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1
+  local rc=$?
+  echo "rc($name)=$rc"; tail -n 2 "gpurun_out/${TAG}_$name.log"
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+has() { [[ ",$PARTS," == *",$1,"* ]]; }
+if has bench; then
+  step bench_c2 300 python bench.py --steps 200 --warmup 20
+  for w in c1 c3 c4; do step bench_$w 300 python bench.py --workload $w --steps 200 --warmup 20; done
+  step bench_c4_strong 300 python bench.py --workload c4 --strong --steps 200 --warmup 20 --no-cpu-baseline
+  step bench_c5 400 python bench.py --workload c5 --steps 50 --warmup 5
+fi
+if has trace; then
+  step trace_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline
+fi
+if has pmc; then
+  # FETCH_SIZE takes 3 of the 4 TCC counters and WRITE_SIZE 2: never in one pass
+  P="FETCH_SIZE|WRITE_SIZE|SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES|SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES|GRBM_GUI_ACTIVE TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"
+  for w in c2 c1 c3; do
+    IFS='|' read -ra PS <<< "$P"; i=0
+    for c in "${PS[@]}"; do i=$((i+1)); step pmc_${w}_p$i 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_$w -o p$i -- python3 tools/prof_one.py --workload $w; done
+  done
+  N="FETCH_SIZE|WRITE_SIZE|TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum|SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES"
+  for m in 15 0; do
+    IFS='|' read -ra PS <<< "$N"; i=0
+    for c in "${PS[@]}"; do i=$((i+1)); step pmc_nat${m}_p$i 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_nat$m -o p$i -- python3 tools/prof_one.py --nat 0 --nat-mask $m; done
+  done
+fi
+if has pmc32; then   # last: a counter this gfx950 image may not have
+  step pmc_nat15_p32 120 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/${TAG}_pmc_nat15 -o p32 -- python3 tools/prof_one.py --nat 0 --nat-mask 15
+fi
+if has host; then
+  step hostpath 400 python tools/hostpath.py
+fi
+echo ALLDONE

@@ -26,7 +26,10 @@ d_arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
 d_desc = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
 V.synth(d_arena, n, stride, 0, V.SYNTH_C2, 0x20241020, 0, d_desc)
 torch.cuda.synchronize()
-h_arena = d_arena.cpu().pin_memory()
+# the arena as a numpy array registered with the context (page-locked + mapped by
+# vpcsum_ctx_register_arena, as a umem would be): the pipeline's MODE_WRITE stores through it
+arena_np = d_arena.cpu().numpy().copy()
+h_arena = torch.from_numpy(arena_np).pin_memory()   # hipHostMalloc'd copy for the zero-copy kernel
 h_desc_t = d_desc.cpu().pin_memory()
 desc = h_desc_t.numpy().view(V.DESC_DTYPE)
 nbytes = algorithmic_bytes(desc)
@@ -37,7 +40,7 @@ ref_np = ref.cpu().numpy().view(np.uint32)
 del d_arena
 
 ctx = V.Context(0, max_arena=(n // 4) * stride + 4096, max_pkts=n // 4)
-arena_np = h_arena.numpy()
+ctx.register(arena_np)
 out = torch.zeros(n, dtype=torch.int32).pin_memory().numpy().view(np.uint32)
 # torch pin_memory() buffers are hipHostMalloc'd: the context recognises them as page-locked
 
@@ -54,6 +57,29 @@ for chunks in (4, 8, 16, 32):
     pipe[chunks] = {"ms": round(dt * 1e3, 3), "GBps_algorithmic": round(nbytes / dt / 1e9, 2),
                     "Mpps": round(n / dt / 1e6, 2)}
 res["pipeline_h2d_kernel_d2h"] = pipe
+
+# the same with the checksum fields written back into the host frames (MODE_WRITE: 2-B posted
+# PCIe writes through the registered arena's mapping)
+want_arena = arena_np.copy()
+pipe = {}
+for chunks in (8, 16):
+    ctx.pipeline(arena_np, stride, 1504, desc, out, mode=V.MODE_WRITE, chunks=chunks)   # warm
+    t = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        ctx.pipeline(arena_np, stride, 1504, desc, out, mode=V.MODE_WRITE, chunks=chunks)
+    dt = (time.perf_counter() - t) / reps
+    assert np.array_equal(out, ref_np)
+    pipe[chunks] = {"ms": round(dt * 1e3, 3), "GBps_algorithmic": round(nbytes / dt / 1e9, 2),
+                    "Mpps": round(n / dt / 1e6, 2)}
+# every frame now carries its sums (verify from the device copy of the written arena)
+d_chk = torch.from_numpy(arena_np).cuda()
+st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+V.compute(d_chk, d_desc, n, None, st, V.MODE_VERIFY)
+torch.cuda.synchronize()
+assert bool(torch.all((st & 3) == 3))
+del d_chk
+res["pipeline_h2d_kernel_d2h_write_frames"] = pipe
 
 # zero-copy: kernel reads the page-locked host arena in place (PCIe reads, no staging copy)
 zc_out = torch.zeros(n, dtype=torch.int32, device="cuda")

@@ -10,16 +10,18 @@ ap.add_argument("--variants", default="0")
 ap.add_argument("--bpc", type=int, default=0)
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--nat", type=int, default=-1, help="nat_mode: profile vpcsum_nat4_async on C5 instead")
+ap.add_argument("--nat-mask", type=int, default=0x0F, help="rewrite mask of every entry (0: read-only pass)")
+ap.add_argument("--nat-n", type=int, default=10_000_000, help="C5 packets (BASELINE: 10M)")
 a = ap.parse_args()
 if a.nat >= 0:
-    n, stride = 10_000_000 // 8, 2048
+    n, stride = a.nat_n, 2048
     arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
     d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
     V.synth(arena, n, stride, 0, V.SYNTH_C5, 0x20241020, 0, d)
     V.compute(arena, d, n, None, None, V.MODE_WRITE)
     g = torch.Generator(device="cpu").manual_seed(5)
     rw = torch.randint(0, 256, (n, 16), dtype=torch.uint8, generator=g)
-    rw[:, 12] = V.NAT_SRC | V.NAT_DST | V.NAT_SPORT | V.NAT_DPORT
+    rw[:, 12] = a.nat_mask
     rw[:, 13:] = 0
     rw = rw.cuda()
     st = torch.zeros(n, dtype=torch.uint8, device="cuda")
