@@ -245,6 +245,25 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint32_t stride, ui
                         uint32_t mode, uint32_t chunks);
 
 /* ------------------------------------------------------------------------ */
+/* Device groups (multi-GPU host batches): one context per GPU in dev_mask;  */
+/* a submitted batch is cut into contiguous descriptor ranges of nearly      */
+/* equal byte totals (prefix sum of l3_len), one per GPU, each processed by  */
+/* its own context; wait joins them.  No data crosses devices.               */
+/* ------------------------------------------------------------------------ */
+typedef struct vpcsum_group vpcsum_group_t;
+int vpcsum_group_create(uint64_t dev_mask, uint64_t max_arena_bytes, uint32_t max_pkts, vpcsum_group_t** out);
+/* devices[0..ndev): a device may repeat (several contexts on one GPU) */
+int vpcsum_group_create_list(const int* devices, int ndev, uint64_t max_arena_bytes, uint32_t max_pkts,
+                             vpcsum_group_t** out);
+int vpcsum_group_destroy(vpcsum_group_t* g);
+/* page-lock once (portable: every GPU of the group maps it) */
+int vpcsum_group_register_arena(vpcsum_group_t* g, void* h_arena, uint64_t len);
+/* as vpcsum_ctx_submit, capacity per GPU; h_out / h_status hold all n results in batch order */
+int vpcsum_group_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                        uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket);
+int vpcsum_group_wait(vpcsum_group_t* g, uint64_t ticket);
+
+/* ------------------------------------------------------------------------ */
 /* PNI entry points (bound by io.vproxy.vpcsum.VPCsum)   */
 /* Layout copied from the PNI convention, base/src/main/c-generated/pni.h   */
 /* ------------------------------------------------------------------------ */

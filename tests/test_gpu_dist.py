@@ -50,3 +50,34 @@ def test_bench_two_ranks_strong(workload):
     assert c["packets_rank0"] < c["global_batch"]
     assert abs(c["algorithmic_bytes_per_step_all_ranks"] - 2 * c["algorithmic_bytes_per_step_rank0"]) \
         < 0.01 * c["algorithmic_bytes_per_step_all_ranks"]
+
+
+@pytest.mark.parametrize("ndev", [1, 3])
+@pytest.mark.parametrize("registered", [False, True])
+def test_device_group_splits_by_bytes(orc, ndev, registered):
+    """vpcsum_group_*: one host batch cut into per-device ranges of nearly equal bytes (three
+    contexts on this box's one GPU stand for three GPUs); results in batch order equal the oracle's,
+    in-place writes land in the caller's frames, two batches can be in flight."""
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import oracle as O
+    from vproxy_amd import vpcsum as V
+    a, d = orc.synth(3000, 9088, 14, O.SYNTH_FUZZ, O.SEED, 77 + ndev)
+    arena = np.concatenate([a, np.zeros(4096, np.uint8)])
+    want, want_st = orc.process(arena, d, O.MODE_VERIFY)
+    g = V.Group([0] * ndev, max_arena=arena.nbytes, max_pkts=len(d))
+    if registered:
+        g.register(arena)
+    out, st = g.run(arena, d, O.MODE_VERIFY)
+    assert np.array_equal(out, want) and np.array_equal(st, want_st)
+    want_arena = arena.copy()
+    wout, _ = orc.process(want_arena, d, O.MODE_COMPUTE, write=True)
+    o1, o2 = np.zeros(1000, np.uint32), np.zeros(2000, np.uint32)
+    t1 = g.submit(arena, d[:1000], o1, None, O.MODE_WRITE)
+    t2 = g.submit(arena, d[1000:], o2, None, O.MODE_WRITE)
+    g.wait(t2)
+    g.wait(t1)
+    assert np.array_equal(np.concatenate([o1, o2]), wout) and np.array_equal(arena, want_arena)
+    g.close()

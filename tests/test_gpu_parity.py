@@ -1090,3 +1090,32 @@ def test_egress_small_flush_hand_back(V, orc):
         batch.defer(int(d["l3_off"]), int(d["l3_len"]), int(d["l4_off"]), 4, int(d["l4_proto"]), int(d["flags"]))
     assert batch.complete_tx() == 8 and np.array_equal(arena, want)
     batch.close()
+
+
+def test_nat_arena_beyond_4gib(V, orc):
+    """NAT on frames placed below and above 4 GiB of a 5-GiB arena (the 10M-packet C5 batch is a
+    20-GB arena): the wide kernel addresses with 64-bit loads and stores, both entry formats."""
+    import torch
+    rng = np.random.default_rng(44)
+    arena, desc, rw = _nat48_batch(orc, rng, 600, 6)
+    n, stride = len(desc), 9088
+    want = arena.copy()
+    orc.nat_java(want, desc, rw)
+    big = torch.zeros((5 << 30) + 4096, dtype=torch.uint8, device="cuda")
+    bases = np.sort(rng.choice(((5 << 30) - (1 << 20)) // 16384, n, replace=False)) * 16384 + 8
+    bases[: n // 3] = np.arange(n // 3) * 16384 + 8
+    dg = desc.copy()
+    src = torch.from_numpy(arena).cuda()
+    for i in range(n):
+        big[int(bases[i]): int(bases[i]) + stride] = src[i * stride:(i + 1) * stride]
+        dg[i]["l3_off"] = int(bases[i]) + int(desc[i]["l3_off"]) - i * stride
+    assert int(dg["l3_off"].max()) > (4 << 30)
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    V.nat(big, V.desc_to_tensor(dg), dev(rw.view(np.uint8)), n, st, V.NAT_RFC1624)
+    torch.cuda.synchronize()
+    assert np.all(st.cpu().numpy() == O.S_DONE)
+    for i in rng.choice(n, 100, replace=False):
+        got = big[int(bases[i]): int(bases[i]) + stride].cpu().numpy()
+        assert np.array_equal(got, want[i * stride:(i + 1) * stride]), i
+    del big
+    torch.cuda.empty_cache()

@@ -30,6 +30,8 @@ if has pmc; then
     IFS='|' read -ra PS <<< "$P"; i=0
     for c in "${PS[@]}"; do i=$((i+1)); step pmc_${w}_p$i 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_$w -o p$i -- python3 tools/prof_one.py --workload $w; done
   done
+fi
+if has pmc || has pmcnat; then
   N="FETCH_SIZE|WRITE_SIZE|TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum|SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES"
   for m in 15 0; do
     IFS='|' read -ra PS <<< "$N"; i=0

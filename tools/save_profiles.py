@@ -1,22 +1,23 @@
-"""Copy the judged evidence of one GPU round (tools/gpu_full.sh) from gpurun_out/ into profiles/
-under a round tag (tooling).  Usage: python tools/save_profiles.py r01c
+"""Copy the judged evidence of one measurement call (tools/gpu_r02.sh <tag>) from gpurun_out/ into
+profiles/ (tooling).  Usage: python tools/save_profiles.py <tag>
 
-  <tag>_c2_kernel_stats.csv     rocprofv3 --kernel-trace --stats of `bench.py` (gpu_round.sh prof)
-  <tag>_bench_<wl>.json         bench.py JSON lines (c2 headline, c1/c3/c4 from gpu_extra.sh)
-  <tag>_pmc_<wl>/pass<i>_k_csum.csv + summary.json   --pmc passes (k_csum* rows) + tools/traffic.py
-  <tag>_nat_c5.json, <tag>_hostpath_c2.json          tools/natbench.py, tools/hostpath.py
+  <tag>_bench_<cfg>.json          bench.py JSON lines (c2 headline; c1 c3 c4 c4_strong c5)
+  <tag>_c2_kernel_stats.csv       rocprofv3 --kernel-trace --stats of `bench.py` (headline command)
+  <tag>_pmc_<cfg>/pass<i>.csv     --pmc passes, rows of the measured kernel only
+  <tag>_pmc_<cfg>/summary.json    per-launch means + HBM bytes (tools/traffic.py rules)
+  <tag>_hostpath_c2.json          tools/hostpath.py
 """
 import csv
 import glob
 import json
 import os
 import shutil
-import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 G = os.path.join(REPO, "gpurun_out")
 P = os.path.join(REPO, "profiles")
+PACKETS = {"c1": 1 << 20, "c2": 1 << 20, "c3": 1 << 20, "c4": 1 << 18}
 
 
 def json_line(log):
@@ -28,40 +29,67 @@ def json_line(log):
     return None
 
 
+def summarise(src, dst, kern, packets):
+    """Mean of each counter over the kernel's dispatches, plus HBM bytes per launch.  Reads: the
+    guide's gfx950 rule for wide streaming reads (FETCH_SIZE counts half: x2); the NAT kernel's
+    reads are scattered 16-48 B header windows, for which the rule is not established, so both
+    the raw and the doubled figure are kept (NAT)."""
+    vals = {}
+    os.makedirs(dst, exist_ok=True)
+    for f in sorted(glob.glob(os.path.join(src, "p*_counter_collection.csv"))):
+        i = os.path.basename(f).split("_")[0][1:]
+        keep = [r for r in csv.DictReader(open(f)) if kern in r["Kernel_Name"]]
+        if not keep:
+            continue
+        with open(os.path.join(dst, f"pass{i}.csv"), "w", newline="") as fo:
+            w = csv.DictWriter(fo, fieldnames=list(keep[0].keys()))
+            w.writeheader()
+            w.writerows(keep)
+        for r in keep:
+            vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    mean = {k: sum(v) / len(v) for k, v in vals.items()}
+    out = {"kernel_substring": kern, "packets": packets, "dispatches": len(vals.get("FETCH_SIZE", [])), **mean}
+    if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+        rd, wr = mean["FETCH_SIZE"] * 1024, mean["WRITE_SIZE"] * 1024
+        out["write_bytes"] = wr
+        if kern == "k_csum":
+            out["read_bytes_corrected"] = 2 * rd
+            out["hbm_bytes_per_launch"] = 2 * rd + wr
+            out["correction"] = "read = 2 x FETCH_SIZE (gfx950 half-count of 128-B streaming requests), MI355X_MICROARCH.md §HBM"
+        else:
+            out["read_bytes_raw"] = rd
+            out["read_bytes_doubled"] = 2 * rd
+            out["hbm_bytes_per_launch"] = rd + wr
+            out["hbm_bytes_per_launch_doubled_reads"] = 2 * rd + wr
+            out["correction"] = ("scattered header windows: FETCH_SIZE taken as is (one 64-B request per "
+                                 "window); the doubled figure is the streaming rule, an upper bound")
+        for k in ("hbm_bytes_per_launch", "write_bytes"):
+            out[k + "_per_packet"] = round(out[k] / packets, 2)
+    for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "TCC_EA0_RDREQ_sum", "TCC_EA0_WRREQ_sum"):
+        if k in mean:
+            out[k + "_per_packet"] = round(mean[k] / packets, 3)
+    json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+
+
 def main(tag):
     os.makedirs(P, exist_ok=True)
-    ks = os.path.join(G, "prof", "run_kernel_stats.csv")
+    for cfg in ("c2", "c1", "c3", "c4", "c4_strong", "c5"):
+        d = json_line(os.path.join(G, f"{tag}_bench_{cfg}.log"))
+        if d:
+            json.dump(d, open(os.path.join(P, f"{tag}_bench_{cfg}.json"), "w"), indent=1)
+    ks = os.path.join(G, f"{tag}_trace", "run_kernel_stats.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(P, f"{tag}_c2_kernel_stats.csv"))
-    for wl, log in (("c2", "bench.log"), ("c1", "bench_c1.log"), ("c3", "bench_c3.log"), ("c4", "bench_c4.log")):
-        d = json_line(os.path.join(G, log))
-        if d:
-            json.dump(d, open(os.path.join(P, f"{tag}_bench_{wl}.json"), "w"))
-    for name, out in (("natbench.log", "nat_c5"), ("hostpath.log", "hostpath_c2"),
-                      ("pattern_all.log", "pattern_ceiling"), ("bench_2rank.log", "bench_2rank_1gpu")):
-        d = json_line(os.path.join(G, name))
-        if d:
-            json.dump(d, open(os.path.join(P, f"{tag}_{out}.json"), "w"), indent=1)
-    fl = os.path.join(G, "flush_latency.json")
-    if os.path.exists(fl) and json_line(fl):
-        json.dump(json_line(fl), open(os.path.join(P, f"{tag}_flush_latency.json"), "w"), indent=1)
-    for src in sorted(glob.glob(os.path.join(G, "pmc_*"))):
-        wl = os.path.basename(src)[4:]
-        kern = "k_nat4w" if wl == "nat" else "k_csum"
-        dst = os.path.join(P, f"{tag}_pmc_{wl}")
-        os.makedirs(dst, exist_ok=True)
-        for f in sorted(glob.glob(os.path.join(src, "p*_counter_collection.csv"))):
-            i = os.path.basename(f).split("_")[0][1:]
-            rows = list(csv.DictReader(open(f)))
-            keep = [r for r in rows if kern in r["Kernel_Name"]]
-            if not keep:
-                continue
-            with open(os.path.join(dst, f"pass{i}_{kern}.csv"), "w", newline="") as fo:
-                w = csv.DictWriter(fo, fieldnames=list(keep[0].keys()))
-                w.writeheader()
-                w.writerows(keep)
-        subprocess.check_call([sys.executable, os.path.join(REPO, "tools", "traffic.py"), dst, kern],
-                              stdout=subprocess.DEVNULL)
+    for src in sorted(glob.glob(os.path.join(G, f"{tag}_pmc_*"))):
+        if not os.path.isdir(src):
+            continue
+        cfg = os.path.basename(src)[len(tag) + 5:]
+        nat = cfg.startswith("nat")
+        summarise(src, os.path.join(P, f"{tag}_pmc_{cfg}"), "vpcsum::k_nat" if nat else "k_csum",
+                  10_000_000 if nat else PACKETS[cfg])
+    d = json_line(os.path.join(G, f"{tag}_hostpath.log"))
+    if d:
+        json.dump(d, open(os.path.join(P, f"{tag}_hostpath_c2.json"), "w"), indent=1)
     print("saved", sorted(f for f in os.listdir(P) if f.startswith(tag)))
 
 

@@ -103,6 +103,7 @@ struct Registered {
     uint8_t* host;
     uint64_t len;
     uint8_t* dev;    // device-side address of the page-locked mapping (zero-copy access)
+    bool owned;      // this context page-locked it (a group's contexts share one registration)
 };
 
 // Zero-copy batches (frames read over PCIe) of at most this many packets run one wave per packet.
@@ -433,7 +434,8 @@ int vpcsum_ctx_destroy(vpcsum_ctx_t* c) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
         slot_free(s);
     }
-    for (auto& r : c->registered) (void)hipHostUnregister(r.host);
+    for (auto& r : c->registered)
+        if (r.owned) (void)hipHostUnregister(r.host);
     delete c;
     return 0;
 }
@@ -449,7 +451,7 @@ int vpcsum_ctx_register_arena(vpcsum_ctx_t* c, void* h_arena, uint64_t len) {
         (void)hipHostUnregister(h_arena);
         return hipfail(e, "hipHostGetDevicePointer");
     }
-    c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev});
+    c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, true});
     return 0;
 }
 
@@ -465,7 +467,7 @@ int vpcsum_ctx_unregister_arena(vpcsum_ctx_t* c, void* h_arena) {
             for (auto& s : c->slots)
                 if (s.busy && s.zero_copy && slot_finish(c, s) != 0) return -1;
             c->svc.par_valid = false;
-            VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
+            if (c->registered[i].owned) VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
             c->registered.erase(c->registered.begin() + i);
             return 0;
         }
@@ -953,6 +955,128 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint
     }
     for (auto& s : c->slots) VPC_CHECK(hipStreamSynchronize(s.stream), "pipeline sync");
     return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Device groups (SURVEY.md §8(b) vpcsum_init(dev_mask), §8(e)): one context per GPU; a host batch
+// is cut into contiguous descriptor ranges of nearly equal byte totals, one per GPU, each run by
+// its own context (own streams, own staging); wait joins them.  No data crosses devices.
+// ------------------------------------------------------------------------------------------
+}  // extern "C"
+
+struct vpcsum_group {
+    std::vector<vpcsum_ctx*> ctx;
+    std::vector<uint8_t*> reg;     // arenas page-locked by the group (portable: every device maps them)
+    uint64_t next_ticket = 1;
+    struct Pending { uint64_t ticket = 0; std::vector<uint64_t> sub; };
+    Pending slots[2];
+    std::mutex mu;
+};
+
+static int vpcsum_group_wait_locked(vpcsum_group* g, vpcsum_group::Pending& slot) {
+    int rc = 0;
+    for (size_t d = 0; d < slot.sub.size(); ++d)
+        if (vpcsum_ctx_wait(g->ctx[d], slot.sub[d]) != 0) rc = -1;   // every device joins, first error kept
+    slot.ticket = 0;
+    return rc;
+}
+
+extern "C" {
+
+int vpcsum_group_create_list(const int* devices, int ndev, uint64_t max_arena_bytes, uint32_t max_pkts,
+                             vpcsum_group_t** out) {
+    if (!out || !devices || ndev <= 0 || ndev > 64) return fail("vpcsum_group_create_list: bad argument");
+    vpcsum_group* g = new vpcsum_group();
+    for (int i = 0; i < ndev; ++i) {
+        vpcsum_ctx_t* c = nullptr;
+        if (vpcsum_ctx_create(devices[i], max_arena_bytes, max_pkts, &c) != 0) {
+            const std::string e = g_err;
+            vpcsum_group_destroy(g);
+            return fail("%s", e.c_str());
+        }
+        g->ctx.push_back(c);
+    }
+    *out = g;
+    return 0;
+}
+
+int vpcsum_group_create(uint64_t dev_mask, uint64_t max_arena_bytes, uint32_t max_pkts, vpcsum_group_t** out) {
+    int n = 0;
+    VPC_CHECK(hipGetDeviceCount(&n), "hipGetDeviceCount");
+    std::vector<int> devs;
+    for (int d = 0; d < 64 && d < n; ++d)
+        if (dev_mask >> d & 1) devs.push_back(d);
+    if (devs.empty() || (n < 64 && (dev_mask >> n) != 0))
+        return fail("vpcsum_group_create: mask 0x%llx names no device or one beyond the %d present",
+                    (unsigned long long)dev_mask, n);
+    return vpcsum_group_create_list(devs.data(), (int)devs.size(), max_arena_bytes, max_pkts, out);
+}
+
+int vpcsum_group_destroy(vpcsum_group_t* g) {
+    if (!g) return 0;
+    for (auto* c : g->ctx) vpcsum_ctx_destroy(c);
+    for (auto* h : g->reg) (void)hipHostUnregister(h);
+    delete g;
+    return 0;
+}
+
+int vpcsum_group_register_arena(vpcsum_group_t* g, void* h_arena, uint64_t len) {
+    if (!g || !h_arena || len == 0) return fail("vpcsum_group_register_arena: bad argument");
+    std::lock_guard<std::mutex> lk(g->mu);
+    VPC_CHECK(hipSetDevice(g->ctx[0]->device), "hipSetDevice");
+    VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterMapped | hipHostRegisterPortable), "hipHostRegister");
+    g->reg.push_back((uint8_t*)h_arena);
+    for (auto* c : g->ctx) {
+        std::lock_guard<std::mutex> lc(c->mu);
+        void* dev = nullptr;
+        VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+        VPC_CHECK(hipHostGetDevicePointer(&dev, h_arena, 0), "hipHostGetDevicePointer");
+        c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, false});
+    }
+    return 0;
+}
+
+int vpcsum_group_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                        uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket) {
+    if (!g || !ticket) return fail("vpcsum_group_submit: NULL group or ticket");
+    if (n && (!h_arena || !h_desc)) return fail("vpcsum_group_submit: NULL arena or descriptors");
+    std::lock_guard<std::mutex> lk(g->mu);
+    const uint64_t t = g->next_ticket++;
+    auto& slot = g->slots[t & 1];
+    if (slot.ticket && vpcsum_group_wait_locked(g, slot) != 0) return -1;
+    // byte-balanced contiguous cuts (shard_by_bytes in vproxy_amd/shard.py)
+    const size_t k = g->ctx.size();
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += h_desc[i].l3_len;
+    std::vector<uint32_t> cut(k + 1, n);
+    cut[0] = 0;
+    uint64_t acc = 0;
+    size_t r = 1;
+    for (uint32_t i = 0; i < n && r < k; ++i) {
+        acc += h_desc[i].l3_len;
+        while (r < k && acc * k >= total * r) cut[r++] = i + 1;
+    }
+    slot.sub.assign(k, 0);
+    for (size_t d = 0; d < k; ++d) {
+        const uint32_t a = cut[d], b = std::max(cut[d], cut[d + 1]);
+        if (vpcsum_ctx_submit(g->ctx[d], h_arena, arena_len, h_desc + a, b - a, h_out ? h_out + a : nullptr,
+                              h_status ? h_status + a : nullptr, mode, &slot.sub[d]) != 0)
+            return -1;
+    }
+    slot.ticket = t;
+    *ticket = t;
+    return 0;
+}
+
+int vpcsum_group_wait(vpcsum_group_t* g, uint64_t ticket) {
+    if (!g) return fail("vpcsum_group_wait: NULL group");
+    std::lock_guard<std::mutex> lk(g->mu);
+    auto& slot = g->slots[ticket & 1];
+    if (slot.ticket != ticket) {
+        if (ticket == 0 || ticket >= g->next_ticket) return fail("vpcsum_group_wait: unknown ticket %llu", (unsigned long long)ticket);
+        return 0;   // already completed
+    }
+    return vpcsum_group_wait_locked(g, slot);
 }
 
 // ------------------------------------------------------------------------------------------

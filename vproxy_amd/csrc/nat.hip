@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void k_nat(uint8_t* __restrict__ arena, uint64
 
 // Wide form: the window [align16(L3), align16(L3) + 96) holding every byte a rewrite touches --
 // the header, the ports and the L4 checksum field of IPv4 with options or IPv6 without extension
-// headers -- is read with up to six 16-B buffer loads (only the chunks the packet needs), staged
+// headers -- is read with up to six 16-B global loads (only the chunks the packet needs), staged
 // in this lane's LDS slot, rewritten there with byte-addressed LDS ops (the window's offset
 // differs per packet), and the changed range is stored back as ONE run of dwordx4 / x2 / dword
 // stores (bytewise only where it would pass the packet end: the next bytes may be another
@@ -253,9 +253,8 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
                                              const uint4* __restrict__ desc, const void* __restrict__ rw, uint32_t n,
                                              uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const v4u gv4u;
     __shared__ uint32_t s_win[256 * kNatSlotDw];
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
     uint32_t* slot = &s_win[threadIdx.x * kNatSlotDw];
     uint8_t* w = (uint8_t*)slot;
     const uint32_t T = gridDim.x * blockDim.x;
@@ -276,15 +275,21 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
             const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
             const int len = dv[i].z & 0xffff, l4o = dv[i].z >> 16;
             const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
-            const int r0 = (int)(off & 15);
+            const bool ok = p < n && nat_desc_ok(off, len, l4o, ver, arena_len, FMT);
+            // the window starts at the 16-B aligned address below the L3 header (absolute: any
+            // arena alignment, any arena size -- 64-bit global loads)
+            const uintptr_t la = ok ? (uintptr_t)(arena + off) : 0;
+            const int r0 = (int)(la & 15);
             int need = ver == 4 ? 20 : 40;
             if (nat_l4sum(ver, proto, len, l4o)) need = max(need, l4o + l4_field(proto) + 2);
-            wend[i] = p < n && nat_desc_ok(off, len, l4o, ver, arena_len, FMT) && r0 + need <= 16 * kNatChunks
-                          ? r0 + need : 0;   // 0: the packet takes the byte-access path
-            const uint32_t boff = (uint32_t)(off - (uint64_t)r0);
+            wend[i] = ok && r0 + need <= 16 * kNatChunks ? r0 + need : 0;   // 0: the byte-access path
+            const uintptr_t base = la - (uintptr_t)r0;
 #pragma unroll
             for (int k = 0; k < kNatChunks; ++k) {
-                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (k << 4) < wend[i] ? boff + (k << 4) : kOutOfRange, 0, 0);
+                // only the chunks the packet needs: all lie in its 16-B blocks, which never cross
+                // a page, so none reads past the arena's last page
+                v4u x = {0u, 0u, 0u, 0u};
+                if ((k << 4) < wend[i]) x = *(gv4u*)(base + 16 * k);
                 v[i][k] = make_uint4(x.x, x.y, x.z, x.w);
             }
         }
@@ -299,8 +304,9 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
             const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
             const int len = dv[i].z & 0xffff, l4o = dv[i].z >> 16;
             const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
-            const int r0 = (int)(off & 15);
-            const uint32_t boff = (uint32_t)(off - (uint64_t)r0);
+            const uintptr_t la = (uintptr_t)(arena + off);
+            const int r0 = (int)(la & 15);
+            uint8_t* base = (uint8_t*)(la - (uintptr_t)r0);
 #pragma unroll
             for (int k = 0; k < kNatChunks; ++k) {
                 if ((k << 4) < wend[i]) {
@@ -319,7 +325,7 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
                 const int jfull = lim >> 2;   // dwords below this lie inside the packet
                 typedef __attribute__((address_space(1))) uint32_t g32;
                 while (j < je) {
-                    uint8_t* dst = arena + boff + 4 * j;
+                    uint8_t* dst = base + 4 * j;
                     if (!(j & 3) && j + 4 <= je && j + 4 <= jfull) {
                         const v4u q = {slot[j], slot[j + 1], slot[j + 2], slot[j + 3]};
                         *(__attribute__((address_space(1))) v4u*)dst = q;
@@ -333,7 +339,7 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
                         *(g32*)dst = slot[j];
                         j += 1;
                     } else {
-                        for (int q = 4 * j; q < lim; ++q) arena[boff + q] = w[q];
+                        for (int q = 4 * j; q < lim; ++q) base[q] = w[q];
                         j += 1;
                     }
                 }
@@ -365,7 +371,7 @@ hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d
     const uint32_t cap = (uint32_t)num_cus(dev) * 8;
     if (g > cap) g = cap;
     // nat_mode bit 8 (internal tuning): force the byte-access kernel
-    const bool wide = !(nat_mode & 0x100u) && arena_len <= kMaxBufArena && !((uintptr_t)arena & 15);
+    const bool wide = !(nat_mode & 0x100u);
     const uint4* d = (const uint4*)desc;
     if (wide) {
 #define VPC_NAT(F, S, W) hipLaunchKernelGGL((k_natw<F, S, W>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out)

@@ -40,6 +40,8 @@ EXPORTS = [
     "vpcsum_ctx_register_arena", "vpcsum_ctx_unregister_arena", "vpcsum_ctx_submit", "vpcsum_ctx_wait",
     "vpcsum_ctx_pipeline", "vpcsum_ctx_set_service", "vpcsum_ctx_stats", "vpcsum_ctx_verify_frames",
     "vpcsum_ctx_nat_submit", "Java_io_vproxy_vpcsum_VPCsum_natSubmit",
+    "vpcsum_group_create", "vpcsum_group_create_list", "vpcsum_group_destroy", "vpcsum_group_register_arena",
+    "vpcsum_group_submit", "vpcsum_group_wait",
     "Java_io_vproxy_vpcsum_VPCsum_create", "Java_io_vproxy_vpcsum_VPCsum_registerArena",
     "Java_io_vproxy_vpcsum_VPCsum_submit", "Java_io_vproxy_vpcsum_VPCsum_waitFor",
     "Java_io_vproxy_vpcsum_VPCsum_close", "Java_io_vproxy_vpcsum_VPCsum_setService",
@@ -70,6 +72,12 @@ def _declare(L):
         "vpcsum_nat4_async": ([P, U64, P, P, U32, P, U32, P], I),
         "vpcsum_nat_async": ([P, U64, P, P, U32, P, U32, P], I),
         "vpcsum_ctx_nat_submit": ([P, P, U64, P, P, U32, P, U32, P], I),
+        "vpcsum_group_create": ([U64, U64, U32, P], I),
+        "vpcsum_group_create_list": ([P, I, U64, U32, P], I),
+        "vpcsum_group_destroy": ([P], I),
+        "vpcsum_group_register_arena": ([P, P, U64], I),
+        "vpcsum_group_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
+        "vpcsum_group_wait": ([P, U64], I),
         "vpcsum_parse_ether_async": ([P, U64, P, P, U32, U8, P, P, P], I),
         "vpcsum_read_probe_async": ([P, U64, P, U32, P], I),
         "vpcsum_pattern_probe_async": ([P, U64, P, U32, P, U32, P], I),
@@ -302,6 +310,55 @@ class Context:
     def close(self):
         if self.h:
             lib().vpcsum_ctx_destroy(self.h)
+            self.h = None
+            self._pinned.clear()
+            self._inflight.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Group:
+    """Several GPUs behind one host batch (vpcsum_group_*): the batch is cut by bytes into one
+    contiguous range per device.  `devices` may repeat a device (several contexts on one GPU)."""
+
+    def __init__(self, devices=(0,), max_arena: int = 1 << 26, max_pkts: int = 1 << 16):
+        h = ctypes.c_void_p()
+        arr = (ctypes.c_int * len(devices))(*devices)
+        _check(lib().vpcsum_group_create_list(arr, len(devices), max_arena, max_pkts, ctypes.byref(h)),
+               "vpcsum_group_create_list")
+        self.h = h.value
+        self._pinned = {}
+        self._inflight = {}
+
+    def register(self, arr: np.ndarray):
+        _check(lib().vpcsum_group_register_arena(self.h, arr.ctypes.data, arr.nbytes), "vpcsum_group_register_arena")
+        self._pinned[arr.ctypes.data] = arr
+
+    def submit(self, arena: np.ndarray, desc: np.ndarray, out: np.ndarray, status: np.ndarray | None = None,
+               mode: int = MODE_COMPUTE) -> int:
+        t = ctypes.c_uint64()
+        _check(lib().vpcsum_group_submit(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data, len(desc),
+                                         out.ctypes.data, None if status is None else status.ctypes.data, mode,
+                                         ctypes.byref(t)), "vpcsum_group_submit")
+        self._inflight[t.value & 1] = (arena, desc, out, status)
+        return t.value
+
+    def wait(self, ticket: int):
+        _check(lib().vpcsum_group_wait(self.h, ticket), "vpcsum_group_wait")
+
+    def run(self, arena, desc, mode: int = MODE_COMPUTE):
+        out = np.zeros(len(desc), np.uint32)
+        status = np.zeros(len(desc), np.uint8)
+        self.wait(self.submit(arena, desc, out, status, mode))
+        return out, status
+
+    def close(self):
+        if self.h:
+            lib().vpcsum_group_destroy(self.h)
             self.h = None
             self._pinned.clear()
             self._inflight.clear()
