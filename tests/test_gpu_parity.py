@@ -1119,3 +1119,5 @@ def test_nat_arena_beyond_4gib(V, orc):
         assert np.array_equal(got, want[i * stride:(i + 1) * stride]), i
     del big
     torch.cuda.empty_cache()
+
+

@@ -82,6 +82,179 @@ struct PktPlan {
     int pslo, pshi;         // pseudo-header address bytes (rel); empty if none
 };
 
+// One packet streamed by a team of TEAM lanes (tl = this lane's index in the team): the body of
+// k1_run.
+template <int TEAM, int U, bool VERIFY, bool NT, bool PRED = false>
+__device__ __forceinline__ void k1_packet(const uint8_t* __restrict__ arena, uint64_t arena_len, const uint4 dv,
+                                          const int fov, const bool has_override, const uint32_t p,
+                                          uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                          uint8_t* __restrict__ arena_w, const int tl) {
+    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+    const int len = dv.z & 0xffff;
+    const int l4o = dv.z >> 16;
+    const int ver = dv.w & 0xff;
+    const int proto = (dv.w >> 8) & 0xff;
+    int fl = (dv.w >> 16) & 0xff;
+    if (has_override) fl = fov;
+
+    // ---- validate (never read or write outside the arena) ----
+    bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
+    const bool raw = (fl & VPCSUM_F_RAW) != 0;
+    bool do_ip = false, do_l4 = false, psonly = false;
+    int fld = -1;
+    if (!bad && !raw) {
+        if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
+        else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
+        else bad = true;
+        if (!bad && (fl & (VPCSUM_F_L4 | VPCSUM_F_L4P))) {
+            psonly = (fl & VPCSUM_F_L4P) != 0;
+            fld = l4_field(proto);
+            if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
+            else if (psonly && ((fl & VPCSUM_F_L4) || proto == 1)) bad = true;
+            else do_l4 = true;
+        }
+        if (!bad && (fl & VPCSUM_F_IP)) {
+            if (ver != 4) bad = true;
+            else do_ip = true;
+        }
+    }
+    if (bad) {
+        if (tl == 0) {
+            if (out) out[p] = 0;
+            if (status) status[p] = VPCSUM_S_BAD_DESC;
+        }
+        return;
+    }
+
+    const uint8_t* l3 = arena + off;
+    const uint4* base = (const uint4*)((uintptr_t)l3 & ~(uintptr_t)15);
+    PktPlan pl;
+    pl.r0 = (int)((uintptr_t)l3 & 15);
+    // pseudo-only (F_L4P): the IP header holds the pseudo addresses, the segment is not read
+    const int need = psonly ? l4o + fld + 2 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
+    pl.nch = (pl.r0 + need + 15) >> 4;
+    if (raw) {
+        pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
+        pl.fast_lo = (pl.r0 + 15) & ~15;
+    } else if (psonly) {
+        pl.l4lo = 0; pl.l4hi = 0; pl.fa = pl.r0 + l4o + fld;
+        pl.fast_lo = 1 << 30;
+    } else if (do_l4) {
+        pl.l4lo = pl.r0 + l4o; pl.l4hi = pl.r0 + len; pl.fa = pl.r0 + l4o + fld;
+        pl.fast_lo = (pl.fa + 2 + 15) & ~15;
+    } else {
+        pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
+        pl.fast_lo = 1 << 30;
+    }
+    pl.fast_hi = (pl.r0 + need) & ~15;
+    if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
+    if (do_l4 && proto != 1) {
+        pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
+        pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
+    } else { pl.pslo = 0; pl.pshi = 0; }
+
+    uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
+    uint32_t st_ip = 0, st_l4 = 0;   // stored fields (verify), as masked LE bytes
+
+    for (int r0 = 0; r0 * TEAM < pl.nch; r0 += U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            // unconditional load (index clamped to the last chunk, a cache hit) keeps the
+            // U loads branch-free and in flight together; out-of-range chunks are skipped below
+            if (PRED) {
+                const int k = (r0 + u) * TEAM + tl;
+                v[u] = k < pl.nch ? ld_stream<NT>(base + k) : make_uint4(0, 0, 0, 0);
+            } else {
+                const int k = min((r0 + u) * TEAM + tl, pl.nch - 1);
+                v[u] = ld_stream<NT>(base + k);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = (r0 + u) * TEAM + tl;
+            if (k >= pl.nch) continue;
+            const int c = k << 4;
+            if (c >= pl.fast_lo && c + 16 <= pl.fast_hi) {
+                // payload chunk: every byte belongs to the L4 sum
+                acc_l4 += (uint64_t)v[u].x + v[u].y;
+                acc_l4 += (uint64_t)v[u].z + v[u].w;
+            } else if (c >= pl.fast_lo) {
+                // tail chunk: past the header and the checksum field, only the end is cut
+                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
+            } else {
+                // header chunk: IPv4 header / pseudo addresses / L4 header / fields
+                const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int d = c + 4 * j;
+                    const uint32_t mf = bmask(d, pl.fa, pl.fa + 2);
+                    acc_l4 += w[j] & bmask(d, pl.l4lo, pl.l4hi) & ~mf;
+                    const uint32_t mif = bmask(d, pl.r0 + 10, pl.r0 + 12);
+                    acc_ip += w[j] & bmask(d, pl.iplo, pl.iphi) & ~mif;
+                    acc_ps += w[j] & bmask(d, pl.pslo, pl.pshi);
+                    if (VERIFY) {
+                        st_l4 += w[j] & mf;
+                        st_ip += (w[j] & mif) & (do_ip ? 0xffffffffu : 0u);
+                    }
+                }
+            }
+        }
+    }
+
+    uint32_t s_l4 = team_sum<TEAM>(fold64(acc_l4));
+    uint32_t s_ip = team_sum<TEAM>(fold64(acc_ip));
+    uint32_t s_ps = team_sum<TEAM>(fold64(acc_ps));
+    uint32_t s_stl4 = 0, s_stip = 0;
+    if (VERIFY) {
+        s_stl4 = team_sum<TEAM>(fold32(st_l4));
+        s_stip = team_sum<TEAM>(fold32(st_ip));
+    }
+
+    if (tl == 0) {
+        uint32_t ipc = 0, l4c = 0;
+        uint8_t st = VPCSUM_S_DONE;
+        if (raw) {
+            ipc = 0xffff - orient(fold32(s_l4), pl.r0);
+        } else {
+            if (do_ip) {
+                ipc = 0xffff - orient(fold32(s_ip), pl.r0);
+            }
+            if (do_l4) {
+                uint32_t tot = orient(fold32(s_l4), pl.r0 + l4o);
+                if (proto != 1) {
+                    const uint32_t l4len = (uint32_t)(len - l4o);
+                    const int pproto = proto;   // Consts.IP_PROTOCOL_* of the L4 class
+                    tot += orient(fold32(s_ps), pl.r0) + (uint32_t)pproto + (l4len & 0xffff) + (l4len >> 16);
+                }
+                if (psonly) {
+                    l4c = fold32(tot);   // CHECKSUM_PARTIAL: uncomplemented
+                } else {
+                    l4c = 0xffff - fold32(tot);
+                    if (proto == 17 && l4c == 0) l4c = 0xffff;
+                }
+            }
+            if (VERIFY) {
+                if (do_ip && orient(fold32(s_stip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
+                if (do_l4) {
+                    const uint32_t stored = orient(fold32(s_stl4), pl.fa);
+                    if (stored == l4c) st |= VPCSUM_S_L4_OK;
+                    if (!psonly && proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                }
+            }
+            if (arena_w) {
+                uint8_t* w = arena_w + off;
+                if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
+                if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
+            }
+        }
+        if (out) out[p] = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
+        if (status) status[p] = st;
+    }
+}
+
 // Body for workgroup `blk` of a grid of `gdim` workgroups (k_csum: the launch grid;
 // k_csum_service: the persistent service grid, once per batch).
 // PRED: chunks past the packet end are not loaded (exec-masked) instead of re-loading the last
@@ -111,171 +284,8 @@ __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64
             dnext = desc[p + nteams];
             if (flags_override) fnext = flags_override[p + nteams];
         }
-
-        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-        const int len = dv.z & 0xffff;
-        const int l4o = dv.z >> 16;
-        const int ver = dv.w & 0xff;
-        const int proto = (dv.w >> 8) & 0xff;
-        int fl = (dv.w >> 16) & 0xff;
-        if (flags_override) fl = fov;
-
-        // ---- validate (never read or write outside the arena) ----
-        bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
-        const bool raw = (fl & VPCSUM_F_RAW) != 0;
-        bool do_ip = false, do_l4 = false, psonly = false;
-        int fld = -1;
-        if (!bad && !raw) {
-            if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
-            else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
-            else bad = true;
-            if (!bad && (fl & (VPCSUM_F_L4 | VPCSUM_F_L4P))) {
-                psonly = (fl & VPCSUM_F_L4P) != 0;
-                fld = l4_field(proto);
-                if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
-                else if (psonly && ((fl & VPCSUM_F_L4) || proto == 1)) bad = true;
-                else do_l4 = true;
-            }
-            if (!bad && (fl & VPCSUM_F_IP)) {
-                if (ver != 4) bad = true;
-                else do_ip = true;
-            }
-        }
-        if (bad) {
-            if (tl == 0) {
-                if (out) out[p] = 0;
-                if (status) status[p] = VPCSUM_S_BAD_DESC;
-            }
-            continue;
-        }
-
-        const uint8_t* l3 = arena + off;
-        const uint4* base = (const uint4*)((uintptr_t)l3 & ~(uintptr_t)15);
-        PktPlan pl;
-        pl.r0 = (int)((uintptr_t)l3 & 15);
-        // pseudo-only (F_L4P): the IP header holds the pseudo addresses, the segment is not read
-        const int need = psonly ? l4o + fld + 2 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
-        pl.nch = (pl.r0 + need + 15) >> 4;
-        if (raw) {
-            pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
-            pl.fast_lo = (pl.r0 + 15) & ~15;
-        } else if (psonly) {
-            pl.l4lo = 0; pl.l4hi = 0; pl.fa = pl.r0 + l4o + fld;
-            pl.fast_lo = 1 << 30;
-        } else if (do_l4) {
-            pl.l4lo = pl.r0 + l4o; pl.l4hi = pl.r0 + len; pl.fa = pl.r0 + l4o + fld;
-            pl.fast_lo = (pl.fa + 2 + 15) & ~15;
-        } else {
-            pl.l4lo = 0; pl.l4hi = 0; pl.fa = -64;
-            pl.fast_lo = 1 << 30;
-        }
-        pl.fast_hi = (pl.r0 + need) & ~15;
-        if (do_ip) { pl.iplo = pl.r0; pl.iphi = pl.r0 + l4o; } else { pl.iplo = 0; pl.iphi = 0; }
-        if (do_l4 && proto != 1) {
-            pl.pslo = pl.r0 + (ver == 4 ? 12 : 8);
-            pl.pshi = pl.r0 + (ver == 4 ? 20 : 40);
-        } else { pl.pslo = 0; pl.pshi = 0; }
-
-        uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
-        uint32_t st_ip = 0, st_l4 = 0;   // stored fields (verify), as masked LE bytes
-
-        for (int r0 = 0; r0 * TEAM < pl.nch; r0 += U) {
-            uint4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                // unconditional load (index clamped to the last chunk, a cache hit) keeps the
-                // U loads branch-free and in flight together; out-of-range chunks are skipped below
-                if (PRED) {
-                    const int k = (r0 + u) * TEAM + tl;
-                    v[u] = k < pl.nch ? ld_stream<NT>(base + k) : make_uint4(0, 0, 0, 0);
-                } else {
-                    const int k = min((r0 + u) * TEAM + tl, pl.nch - 1);
-                    v[u] = ld_stream<NT>(base + k);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int k = (r0 + u) * TEAM + tl;
-                if (k >= pl.nch) continue;
-                const int c = k << 4;
-                if (c >= pl.fast_lo && c + 16 <= pl.fast_hi) {
-                    // payload chunk: every byte belongs to the L4 sum
-                    acc_l4 += (uint64_t)v[u].x + v[u].y;
-                    acc_l4 += (uint64_t)v[u].z + v[u].w;
-                } else if (c >= pl.fast_lo) {
-                    // tail chunk: past the header and the checksum field, only the end is cut
-                    const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, pl.l4hi);
-                } else {
-                    // header chunk: IPv4 header / pseudo addresses / L4 header / fields
-                    const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int d = c + 4 * j;
-                        const uint32_t mf = bmask(d, pl.fa, pl.fa + 2);
-                        acc_l4 += w[j] & bmask(d, pl.l4lo, pl.l4hi) & ~mf;
-                        const uint32_t mif = bmask(d, pl.r0 + 10, pl.r0 + 12);
-                        acc_ip += w[j] & bmask(d, pl.iplo, pl.iphi) & ~mif;
-                        acc_ps += w[j] & bmask(d, pl.pslo, pl.pshi);
-                        if (VERIFY) {
-                            st_l4 += w[j] & mf;
-                            st_ip += (w[j] & mif) & (do_ip ? 0xffffffffu : 0u);
-                        }
-                    }
-                }
-            }
-        }
-
-        uint32_t s_l4 = team_sum<TEAM>(fold64(acc_l4));
-        uint32_t s_ip = team_sum<TEAM>(fold64(acc_ip));
-        uint32_t s_ps = team_sum<TEAM>(fold64(acc_ps));
-        uint32_t s_stl4 = 0, s_stip = 0;
-        if (VERIFY) {
-            s_stl4 = team_sum<TEAM>(fold32(st_l4));
-            s_stip = team_sum<TEAM>(fold32(st_ip));
-        }
-
-        if (tl == 0) {
-            uint32_t ipc = 0, l4c = 0;
-            uint8_t st = VPCSUM_S_DONE;
-            if (raw) {
-                ipc = 0xffff - orient(fold32(s_l4), pl.r0);
-            } else {
-                if (do_ip) {
-                    ipc = 0xffff - orient(fold32(s_ip), pl.r0);
-                }
-                if (do_l4) {
-                    uint32_t tot = orient(fold32(s_l4), pl.r0 + l4o);
-                    if (proto != 1) {
-                        const uint32_t l4len = (uint32_t)(len - l4o);
-                        const int pproto = proto;   // Consts.IP_PROTOCOL_* of the L4 class
-                        tot += orient(fold32(s_ps), pl.r0) + (uint32_t)pproto + (l4len & 0xffff) + (l4len >> 16);
-                    }
-                    if (psonly) {
-                        l4c = fold32(tot);   // CHECKSUM_PARTIAL: uncomplemented
-                    } else {
-                        l4c = 0xffff - fold32(tot);
-                        if (proto == 17 && l4c == 0) l4c = 0xffff;
-                    }
-                }
-                if (VERIFY) {
-                    if (do_ip && orient(fold32(s_stip), pl.r0) == ipc) st |= VPCSUM_S_IP_OK;
-                    if (do_l4) {
-                        const uint32_t stored = orient(fold32(s_stl4), pl.fa);
-                        if (stored == l4c) st |= VPCSUM_S_L4_OK;
-                        if (!psonly && proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
-                    }
-                }
-                if (arena_w) {
-                    uint8_t* w = arena_w + off;
-                    if (do_ip) { w[10] = (uint8_t)(ipc >> 8); w[11] = (uint8_t)ipc; }
-                    if (do_l4) { w[l4o + fld] = (uint8_t)(l4c >> 8); w[l4o + fld + 1] = (uint8_t)l4c; }
-                }
-            }
-            if (out) out[p] = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
-            if (status) status[p] = st;
-        }
+        k1_packet<TEAM, U, VERIFY, NT, PRED>(arena, arena_len, dv, fov, flags_override != nullptr, p, out, status,
+                                             arena_w, tl);
     }
 }
 
