@@ -44,4 +44,10 @@ fi
 if has host; then
   step hostpath 400 python tools/hostpath.py
 fi
+if has flush; then   # tools/flush_latency is built in-tree beforehand (g++ line in its header)
+  step flush 300 ./tools/flush_latency 2000
+fi
+if has rank2; then   # the multi-rank path rehearsed on one GPU (bench.py launches its own ranks)
+  step bench_c2_2rank 300 python bench.py --gpus 2 --steps 50 --warmup 5 --no-cpu-baseline
+fi
 echo ALLDONE
