@@ -1,16 +1,24 @@
-"""Summarise rocprofv3 --pmc CSVs (per kernel name: mean of each counter over dispatches)."""
-import csv, glob, sys, collections
-d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in sorted(glob.glob(f"{d}/*_counter_collection.csv")):
+"""Mean of each PMC counter per kernel (by template instance) over the passes of
+tools/pmc_variants.sh (tooling).  Usage: python tools/pmc_summary.py gpurun_out/<tag> [packets]"""
+import csv
+import glob
+import os
+import re
+import sys
+
+d = sys.argv[1]
+pk = float(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
+vals = {}
+for f in glob.glob(os.path.join(d, "**", "p*_counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "csum" not in k and "read_probe" not in k:
+        if "k_csum" not in k:
             continue
-        acc[k][(r["Dispatch_Id"], r["Counter_Name"])].append(float(r["Counter_Value"]))
-for k, m in acc.items():
-    per = collections.defaultdict(list)
-    for (disp, c), vals in m.items():
-        per[c].append(sum(vals))
-    short = k.split("(")[0][:70]
-    print(short, {c: f"{sum(v)/len(v):.4g}" for c, v in sorted(per.items())})
+        m = re.search(r"k_csum_d<([^>]*)>", k)
+        key = m.group(1) if m else k[:60]
+        vals.setdefault(key, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+for key, cs in sorted(vals.items()):
+    print(key)
+    for c, v in sorted(cs.items()):
+        m = sum(v) / len(v)
+        print(f"   {c:24s} {m:14.1f}   per pkt {m / pk:9.3f}")

@@ -505,11 +505,95 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
     }
 }
 
+// Window chunk c -> LDS slot: rotated by the 256-B row index within its row, so that lanes
+// reading the chunks of packets 64 B apart (ds_read_b128, 16-lane groups) hit distinct slots,
+// and 8 consecutive lanes writing consecutive chunks (ds_write_b128) still do.
+__device__ __forceinline__ uint32_t win_slot(uint32_t c) { return (c & ~15u) | ((c + (c >> 4)) & 15u); }
+
+// The descriptor rules of K2's phase A that depend on the descriptor's fields alone (bounds,
+// liveness, raw ranges and rejected flags are checked by the caller): IP version and lengths,
+// the L4 checksum field inside the segment, flag combinations.  Wave-uniform arguments give
+// scalar code (window units check lane 0's descriptor once for the whole unit).
+struct DescRules {
+    bool bad, do_ip, do_l4, psonly;
+    int fld;
+};
+__device__ __forceinline__ DescRules desc_rules(int len, int l4o, int ver, int proto, int fl) {
+    DescRules r;
+    r.do_ip = r.do_l4 = r.psonly = false;
+    r.fld = -1;
+    bool bad;
+    if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
+    else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
+    else bad = true;
+    if (!bad && (fl & (VPCSUM_F_L4 | VPCSUM_F_L4P))) {
+        r.psonly = (fl & VPCSUM_F_L4P) != 0;
+        r.fld = l4_field(proto);
+        if (r.fld < 0 || (ver == 4 && proto == 58) || len - l4o < r.fld + 2) bad = true;
+        else if (r.psonly && ((fl & VPCSUM_F_L4) || proto == 1)) bad = true;
+        else r.do_l4 = true;
+    }
+    if (!bad && (fl & VPCSUM_F_IP)) {
+        if (ver != 4) bad = true;
+        else r.do_ip = true;
+    }
+    r.bad = bad;
+    return r;
+}
+
+// Sums of a window unit's packet in K2's slot format {l4, ip, 0, stored l4 | stored ip << 16}
+// from x = the packet's chunks (20 dwords from its chunk-aligned start).  L3 starts at dword Q
+// + sh bytes (sh 0 or 2: even offsets only), so a[k] = alignbyte(x[Q+k+1], x[Q+k], sh) is L3
+// dword k, little-endian, and with IPv4 of 20 B or IPv6 of 40 B every field is at a fixed
+// dword: IP checksum a[2] high half, pseudo addresses a[3..4] / a[2..9], the L4 checksum at
+// l4o + fld.  Bytes past the packet (a neighbour's) are masked off at dword nd - 1 and beyond.
+// An even start gives the sums the same byte orientation as K2's chunk-aligned ones.
+template <int Q, bool VERIFY>
+__device__ __forceinline__ uint4 win_sums(const uint32_t (&x)[20], int sh, int ver, int proto, int len, int fl) {
+    uint32_t a[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a[k] = __builtin_amdgcn_alignbyte(x[Q + k + 1], x[Q + k], (uint32_t)sh);
+    const bool do_ip = (fl & VPCSUM_F_IP) != 0;
+    const bool psonly = (fl & VPCSUM_F_L4P) != 0;
+    const bool do_l4 = (fl & (VPCSUM_F_L4 | VPCSUM_F_L4P)) != 0;
+    const int l4d = ver == 4 ? 5 : 10;
+    const int nd = (len + 3) >> 2;
+    const uint32_t tail = (len & 3) ? (0xffffffffu >> (8 * (4 - (len & 3)))) : 0xffffffffu;
+    uint64_t ip = 0, l4 = 0;
+    uint32_t st_ip = 0, st_l4 = 0;
+    if (do_ip) {   // IPv4 only (checked with the descriptor)
+        ip = (uint64_t)a[0] + a[1] + (a[2] & 0xffffu) + a[3] + a[4];
+        st_ip = a[2] >> 16;
+    }
+    if (do_l4) {
+        const int fo = 4 * l4d + l4_field(proto);   // L4 checksum field, bytes from L3
+        const int fd = fo >> 2;
+        const uint32_t fkeep = (fo & 2) ? 0x0000ffffu : 0xffff0000u;
+        if (proto != 1) {
+            if (ver == 4) l4 = (uint64_t)a[3] + a[4];
+            else l4 = (uint64_t)a[2] + a[3] + a[4] + a[5] + a[6] + a[7] + a[8] + a[9];
+        }
+#pragma unroll
+        for (int k = 5; k < 16; ++k) {
+            if (k >= l4d && k < nd) {
+                uint32_t w = a[k];
+                if (k == nd - 1) w &= tail;
+                if (k == fd) {
+                    st_l4 = (fo & 2) ? w >> 16 : w & 0xffffu;
+                    w &= fkeep;
+                }
+                if (!psonly) l4 += w;
+            }
+        }
+    }
+    return make_uint4(fold32(fold64(l4)), fold32(fold64(ip)), 0u, VERIFY ? (st_l4 | (st_ip << 16)) : 0u);
+}
+
 // K2 body for workgroup `blk` of a grid of `gdim` workgroups (k_csum_d: the launch grid;
 // k_csum_service: the persistent service grid, once per batch).
 // ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
 // ROT > 0 rotates whole iterations (64 / TEAM packets), ROT < 0 single slots.
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false>
 __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -559,6 +643,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     // first descriptor in registers before the loop, so that the loop head holds no wait that
     // the back edge (this unit's stores pending) would have to honour too
     asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     for (uint32_t Pn; P0 < n; P0 = Pn) {
         // ---- phase A: this lane's packet ----
         const uint4 dv = dnext;
@@ -579,30 +664,93 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         const int proto = (dv.w >> 8) & 0xff;
         const int fl = flags_override ? fov : (int)((dv.w >> 16) & 0xff);
 
-        bool bad = !live || off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
-        const bool raw = (fl & VPCSUM_F_RAW) != 0;
-        bool do_ip = false, do_l4 = false, psonly = false;
-        int fld = -1;
-        if (!bad && !raw) {
-            if (ver == 4) bad = len < 20 || l4o < 20 || l4o > len || (l4o & 3);
-            else if (ver == 6) bad = len < 40 || l4o < 40 || l4o > len;
-            else bad = true;
-            if (!bad && (fl & (VPCSUM_F_L4 | VPCSUM_F_L4P))) {
-                psonly = (fl & VPCSUM_F_L4P) != 0;
-                fld = l4_field(proto);
-                if (fld < 0 || (ver == 4 && proto == 58) || len - l4o < fld + 2) bad = true;
-                else if (psonly && ((fl & VPCSUM_F_L4) || proto == 1)) bad = true;
-                else do_l4 = true;
-            }
-            if (!bad && (fl & VPCSUM_F_IP)) {
-                if (ver != 4) bad = true;
-                else do_ip = true;
-            }
-        }
         const int r0 = (int)(off & 15);
+        // this lane's descriptor: set by the window check (one scalar check of lane 0's
+        // descriptor for the whole unit) or by the per-lane decode below
+        bool bad = true, raw = false, do_ip = false, do_l4 = false, psonly = false;
+        int fld = -1;
         int key = 0;
         int n_small = 0, n_cls = 0;   // n_cls: distinct cost classes in the large tier
-        {
+        bool fastu = false;           // window unit (SF): sums in fsums, no slots
+        uint4 fsums = make_uint4(0, 0, 0, 0);
+        // Window units (SF): the 64 packets of the unit have one shape (descriptor fields, flags
+        // and L3 alignment equal to lane 0's: IPv4 without options or IPv6 without extension
+        // headers, L3 <= 64 B at an even offset) and lie in 4 KB from lane 0's first chunk, lane
+        // 63 last.  The wave reads that window with coalesced 16-B loads (one round trip, 1 KB
+        // per instruction) into its LDS slots, and every lane sums its own packet from L3-aligned
+        // dwords, where the header fields sit at fixed dwords: no plan, no sort, no team
+        // reduction, no per-dword masks.  The sums have K2's slot format.
+        if (SF) {
+            const uint32_t boff = (uint32_t)off & ~15u;
+            const uint32_t base = __builtin_amdgcn_readfirstlane(boff);
+            const uint32_t rel = boff - base;
+            const uint32_t u_rel63 = __builtin_amdgcn_readlane(rel, 63);
+            const uint32_t kd = (dv.w & 0xffffu) | ((uint32_t)fl << 16) | ((uint32_t)r0 << 24);
+            const uint32_t u_z = __builtin_amdgcn_readfirstlane(dv.z), u_kd = __builtin_amdgcn_readfirstlane(kd);
+            const bool cand = live && off <= arena_len && (uint64_t)len <= arena_len - off &&
+                              !(fl & (kFlagRejected | VPCSUM_F_RAW)) && dv.z == u_z && kd == u_kd && rel <= u_rel63;
+            if (__ballot(cand) == ~0ull) {
+                const int u_len = (int)(u_z & 0xffff), u_l4o = (int)(u_z >> 16);
+                const int u_ver = (int)(u_kd & 0xff), u_r0 = (int)(u_kd >> 24);
+                const DescRules ur = desc_rules(u_len, u_l4o, u_ver, (int)((u_kd >> 8) & 0xff), (int)((u_kd >> 16) & 0xff));
+                const uint32_t hiw = u_rel63 + (uint32_t)((u_r0 + u_len + 15) & ~15);   // bytes of the window
+                if (!ur.bad && !(u_r0 & 1) && u_len <= 64 && ((u_ver == 4 && u_l4o == 20) || (u_ver == 6 && u_l4o == 40)) &&
+                    hiw <= 4096u) {
+                    fastu = true;
+                    bad = false;
+                    do_ip = ur.do_ip;
+                    do_l4 = ur.do_l4;
+                    psonly = ur.psonly;
+                    fld = ur.fld;
+                    v4u* win = (v4u*)&s_slot[wid][0][0];
+                    // lane index through an opaque copy: the window addresses below are the same
+                    // in every unit, and hoisted out of the unit loop they would stay live across
+                    // the large tier's phase B (+20 VGPRs, one wave per SIMD less)
+                    uint32_t ln = (uint32_t)lane;
+                    asm volatile("" : "+v"(ln));
+                    {
+                        v4u c[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint32_t cb = (64u * u + ln) << 4;
+                            c[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, cb < hiw ? base + cb : kOutOfRange, 0, NT ? 2 : 0);
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) win[win_slot(64u * u + ln)] = c[u];
+                    }
+                    wave_sync_lds();
+                    // this lane's chunks [c0, c0 + 5): 20 dwords from its chunk-aligned start
+                    uint32_t x[20];
+                    const uint32_t c0 = rel >> 4;
+                    const int nchw = (u_r0 + u_len + 15) >> 4;
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) {
+                        v4u v = v4u{0, 0, 0, 0};
+                        if (k < nchw) v = win[win_slot(c0 + (uint32_t)k)];
+                        x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+                    }
+                    const int u_fl = (int)((u_kd >> 16) & 0xff), u_proto = (int)((u_kd >> 8) & 0xff);
+                    const int q = u_r0 >> 2;
+                    if (q == 0) fsums = win_sums<0, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
+                    else if (q == 1) fsums = win_sums<1, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
+                    else if (q == 2) fsums = win_sums<2, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
+                    else fsums = win_sums<3, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
+                }
+            }
+        }
+        if (!fastu) {
+            bad = !live || off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
+            raw = (fl & VPCSUM_F_RAW) != 0;
+            if (!bad && !raw) {
+                const DescRules r = desc_rules(len, l4o, ver, proto, fl);
+                bad = r.bad;
+                do_ip = r.do_ip;
+                do_l4 = r.do_l4;
+                psonly = r.psonly;
+                fld = r.fld;
+            }
+        }
+        if (!fastu) {
             PktPlan pl;
             pl.r0 = r0;
             const uint32_t boff = (uint32_t)(off & ~(uint64_t)15);
@@ -661,15 +809,75 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                 if (b == 1) n_small = (int)cnt;   // keys 0 and 1 go to the small tier
             }
             key = (int)rank;   // from here on: this packet's slot
-            uint4* sl = s_slot[wid][rank];
-            sl[0] = make_uint4(boff, (uint32_t)pl.nch | ((uint32_t)klo << 16) | ((uint32_t)do_ip << 30) | ((uint32_t)fastc << 31),
-                               kfast, (uint32_t)pl.l4hi);
-            sl[1] = make_uint4(B_ip, B_l4, F_ip, F_l4);
-            if (!fastc) {
-                sl[2] = make_uint4((uint32_t)r0, (uint32_t)pl.l4lo, (uint32_t)pl.fa, (uint32_t)pl.iphi);
-                sl[3] = make_uint4((uint32_t)pl.iplo, (uint32_t)pl.pslo, (uint32_t)pl.pshi, 0u);
+            {
+                uint4* sl = s_slot[wid][rank];
+                sl[0] = make_uint4(boff, (uint32_t)pl.nch | ((uint32_t)klo << 16) | ((uint32_t)do_ip << 30) | ((uint32_t)fastc << 31),
+                                   kfast, (uint32_t)pl.l4hi);
+                sl[1] = make_uint4(B_ip, B_l4, F_ip, F_l4);
+                if (!fastc) {
+                    sl[2] = make_uint4((uint32_t)r0, (uint32_t)pl.l4lo, (uint32_t)pl.fa, (uint32_t)pl.iphi);
+                    sl[3] = make_uint4((uint32_t)pl.iplo, (uint32_t)pl.pslo, (uint32_t)pl.pshi, 0u);
+                }
             }
         }
+        // ---- phase C: finalize this lane's packet from its sums {l4, ip, pseudo, stored} ----
+        auto finish = [&](const uint4 sums) {
+            uint32_t res_out = 0, res_st = VPCSUM_S_BAD_DESC;
+            {
+                if (!bad) {
+                    uint32_t ipc = 0, l4c = 0;
+                    uint32_t st = VPCSUM_S_DONE;
+                    if (raw) {
+                        ipc = 0xffff - orient(sums.x, r0);
+                    } else {
+                        if (do_ip) ipc = 0xffff - orient(sums.y, r0);
+                        if (do_l4) {
+                            uint32_t tot = orient(sums.x, r0 + l4o);
+                            if (proto != 1) {
+                                const uint32_t l4len = (uint32_t)(len - l4o);
+                                tot += orient(sums.z, r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
+                            }
+                            if (psonly) {
+                                l4c = fold32(tot);   // CHECKSUM_PARTIAL: uncomplemented
+                            } else {
+                                l4c = 0xffff - fold32(tot);
+                                if (proto == 17 && l4c == 0) l4c = 0xffff;
+                            }
+                        }
+                        if (VERIFY) {
+                            if (do_ip && orient(sums.w >> 16, r0) == ipc) st |= VPCSUM_S_IP_OK;
+                            if (do_l4) {
+                                const uint32_t stored = orient(sums.w & 0xffff, r0 + l4o + fld);
+                                if (stored == l4c) st |= VPCSUM_S_L4_OK;
+                                if (!psonly && proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                            }
+                        }
+                        if (arena_w) {
+                            uint8_t* w = arena_w + off;
+                            if (do_ip) st_be16_nt(w + 10, ipc);
+                            if (do_l4) st_be16_nt(w + l4o + fld, l4c);
+                        }
+                    }
+                    res_out = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
+                    res_st = st;
+                }
+            }
+            if (live) {
+                if (NT) {
+                    if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lo));
+                    if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lo));
+                } else {
+                    if (out) out[P0 + lo] = res_out;
+                    if (status) status[P0 + lo] = (uint8_t)res_st;
+                }
+            }
+        };
+
+        uint4 sums;
+        if (fastu) {
+            asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
+            sums = fsums;
+        } else {
         wave_sync_lds();
 
         // ---- phase B: teams stream the packets in slot order ----
@@ -687,70 +895,21 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         // before this unit's stores: vmcnt counts loads and stores together, so a wait for it
         // after the stores would stall the wave until they complete, once per unit.
         asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
-
-        // ---- phase C: finalize this lane's packet ----
-        uint32_t res_out = 0, res_st = VPCSUM_S_BAD_DESC;
-        {
-            const uint4 sums = s_slot[wid][key][0];
-            if (!bad) {
-                uint32_t ipc = 0, l4c = 0;
-                uint32_t st = VPCSUM_S_DONE;
-                if (raw) {
-                    ipc = 0xffff - orient(sums.x, r0);
-                } else {
-                    if (do_ip) ipc = 0xffff - orient(sums.y, r0);
-                    if (do_l4) {
-                        uint32_t tot = orient(sums.x, r0 + l4o);
-                        if (proto != 1) {
-                            const uint32_t l4len = (uint32_t)(len - l4o);
-                            tot += orient(sums.z, r0) + (uint32_t)proto + (l4len & 0xffff) + (l4len >> 16);
-                        }
-                        if (psonly) {
-                            l4c = fold32(tot);   // CHECKSUM_PARTIAL: uncomplemented
-                        } else {
-                            l4c = 0xffff - fold32(tot);
-                            if (proto == 17 && l4c == 0) l4c = 0xffff;
-                        }
-                    }
-                    if (VERIFY) {
-                        if (do_ip && orient(sums.w >> 16, r0) == ipc) st |= VPCSUM_S_IP_OK;
-                        if (do_l4) {
-                            const uint32_t stored = orient(sums.w & 0xffff, r0 + l4o + fld);
-                            if (stored == l4c) st |= VPCSUM_S_L4_OK;
-                            if (!psonly && proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
-                        }
-                    }
-                    if (arena_w) {
-                        uint8_t* w = arena_w + off;
-                        if (do_ip) st_be16_nt(w + 10, ipc);
-                        if (do_l4) st_be16_nt(w + l4o + fld, l4c);
-                    }
-                }
-                res_out = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
-                res_st = st;
-            }
+        sums = s_slot[wid][key][0];
         }
-        if (live) {
-            if (NT) {
-                if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lo));
-                if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lo));
-            } else {
-                if (out) out[P0 + lo] = res_out;
-                if (status) status[P0 + lo] = (uint8_t)res_st;
-            }
-        }
+        finish(sums);
         wave_sync_lds();   // slots are rewritten by the next super-iteration
     }
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
                                                 uint8_t* __restrict__ arena_w, uint32_t low_grid) {
-    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT>(arena, arena_len, desc, n, out, status, flags_override, arena_w, low_grid,
-                                            blockIdx.x, gridDim.x);
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF>(arena, arena_len, desc, n, out, status, flags_override, arena_w,
+                                                low_grid, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -960,7 +1119,7 @@ static uint32_t default_low_grid() {
     return (uint32_t)num_cus(dev) * 2u;
 }
 
-template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, bool adapt, hipStream_t stream) {
@@ -977,7 +1136,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
+    hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
                        (const uint4*)desc, n, out, status, flags_override, arena_w, low_grid)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -1028,6 +1187,7 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 58: return launch_d<8, 12, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 62: return launch_d<8, 6, 2, 2, 1, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 66: return launch_d<8, 6, 2, 2, 1, 0, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 70: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         default: return hipErrorInvalidValue;   // unknown kernel variant id
     }
