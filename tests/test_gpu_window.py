@@ -14,7 +14,7 @@ from tests.test_gpu_parity import V, gpu_compute  # noqa: F401  (V: the library 
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 70]
+VARIANTS = [0, 72]
 
 # (ver, proto, l3_len, flags): shapes whose r0 + l3_len fits the first 64 B of the chunk-aligned
 # frame for r0 = 14 (l3_len <= 50) or r0 = 0 (<= 64)

@@ -1112,6 +1112,12 @@ static uint32_t default_grid() {
     (void)hipGetDevice(&dev);
     return (uint32_t)num_cus(dev) * 12u;
 }
+// Grid of K2 for dense small frames: 5 workgroups per CU (all resident at 5 waves per SIMD).
+static uint32_t default_dense_grid() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return (uint32_t)num_cus(dev) * 5u;
+}
 // Low-concurrency grid of K2 for batches of large packets: 2 workgroups per CU.
 static uint32_t default_low_grid() {
     int dev = 0;
@@ -1133,6 +1139,10 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     // (otherwise the sample cannot succeed and its load latency would be pure cost)
     const uint32_t low_grid =
         (grid > 0 || IL != 0 || !adapt || arena_len < (uint64_t)n * 1024u) ? 0u : default_low_grid();
+    // Dense small frames (at most 128 arena bytes per packet): 5 workgroups per CU, all resident,
+    // beat the 12 of the grid-stride default (C1 window units: 4.64 vs 4.49 TB/s, DESIGN.md §5
+    // item 16); the arena size alone tells, no sample needed.
+    if (grid <= 0 && adapt && IL == 0 && arena_len <= (uint64_t)n * 128u) g = min(g, default_dense_grid());
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
@@ -1187,8 +1197,10 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 58: return launch_d<8, 12, 2, 2>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 62: return launch_d<8, 6, 2, 2, 1, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 66: return launch_d<8, 6, 2, 2, 1, 0, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
-        case 70: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
-        case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        // 70: the default; 72: the default without window units (A/B)
+        case 72: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 70:
+        case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         default: return hipErrorInvalidValue;   // unknown kernel variant id
     }
 #undef VPC_T
