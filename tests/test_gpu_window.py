@@ -125,3 +125,30 @@ def test_c1_synth_window(V, orc):
     """The C1 generator at its bench stride (64-B frames, L3 at 14), 3000 packets."""
     arena, desc = orc.synth(3000, 64, 14, O.SYNTH_C1, O.SEED, 555)
     check_all(V, orc, arena, desc)
+
+
+@pytest.mark.parametrize("registered", [False, True])
+def test_window_units_host_context(V, orc, registered):
+    """Dense small frames from host memory: staged through the context's device buffers
+    (pageable arena) or read in place from a registered one (zero-copy), verify then write-back;
+    batches large enough that K2 (not the one-wave-per-packet zero-copy variant) runs."""
+    rng = np.random.default_rng(31)
+    arena, desc = build(rng, lambda u, i: SHAPES_14[u % 4], 64 * 40 + 5, 64, 14)
+    good = arena.copy()
+    orc.process(good, desc, O.MODE_COMPUTE, write=True)
+    for i in range(0, len(desc), 7):
+        good[int(desc["l3_off"][i]) + 20] ^= 0x11
+    ctx = V.Context(0, max_arena=good.nbytes, max_pkts=len(desc))
+    try:
+        if registered:
+            ctx.register(good)
+        out, st = ctx.run(good, desc, O.MODE_VERIFY)
+        oout, ost = orc.process(good.copy(), desc, O.MODE_VERIFY)
+        assert np.array_equal(out, oout) and np.array_equal(st, ost)
+        want = good.copy()
+        wout, _ = orc.process(want, desc, O.MODE_COMPUTE, write=True)
+        out = np.zeros(len(desc), np.uint32)
+        ctx.wait(ctx.submit(good, desc, out, None, O.MODE_WRITE))
+        assert np.array_equal(out, wout) and np.array_equal(good, want)
+    finally:
+        ctx.close()
