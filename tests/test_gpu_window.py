@@ -152,3 +152,30 @@ def test_window_units_host_context(V, orc, registered):
         assert np.array_equal(out, wout) and np.array_equal(good, want)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("stride,pad", [(2048, 14), (2048, 0), (4096, 2), (192, 14)])
+def test_gathered_units(V, orc, stride, pad):
+    """Small packets of one shape in sparse frames (2-KB umem frames and others): not within one
+    4-KB window, so the unit's chunks are gathered per packet; shapes of 1 to 4 chunks."""
+    rng = np.random.default_rng(stride + pad)
+    fit = 64 - (pad & 15)
+    shapes = [s for s in SHAPES_0 if s[2] <= fit]
+    arena, desc = build(rng, lambda u, i: shapes[u % len(shapes)], 64 * len(shapes) + 9, stride, pad)
+    check_all(V, orc, arena, desc)
+
+
+def test_gathered_units_shuffled(V, orc):
+    """Descriptors in random order over 64-B frames (not ascending, so not a window), and units
+    whose frames lie in reverse order."""
+    rng = np.random.default_rng(5)
+    arena, desc = build(rng, lambda u, i: SHAPES_14[0], 64 * 12, 64, 14)
+    perm = rng.permutation(len(desc))
+    check_all(V, orc, arena, desc[perm].copy())
+    check_all(V, orc, arena, desc[::-1].copy())
+
+
+def test_c1_synth_umem_frames(V, orc):
+    """The C1 generator in 2-KB frames (the AF_XDP umem layout), 3000 packets."""
+    arena, desc = orc.synth(3000, 2048, 14, O.SYNTH_C1, O.SEED, 77)
+    check_all(V, orc, arena, desc)

@@ -21,9 +21,12 @@ ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--mode", type=int, default=0)
 ap.add_argument("--noout", type=int, default=0)
 ap.add_argument("--full", default="0", help="1 = no sampled low-concurrency grid (K2 tuning bit 14)")
+ap.add_argument("--stride", type=int, default=0, help="frame stride instead of the workload's (e.g. c1 in 2-KB frames)")
 args = ap.parse_args()
 
 sid, n, stride, text = WORKLOADS[args.workload]
+if args.stride:
+    stride, text = args.stride, f"{text}, stride {args.stride}"
 arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
 d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
 V.synth(arena, n, stride, 0, sid, 0x20241020, 0, d)

@@ -688,14 +688,18 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
             const uint32_t kd = (dv.w & 0xffffu) | ((uint32_t)fl << 16) | ((uint32_t)r0 << 24);
             const uint32_t u_z = __builtin_amdgcn_readfirstlane(dv.z), u_kd = __builtin_amdgcn_readfirstlane(kd);
             const bool cand = live && off <= arena_len && (uint64_t)len <= arena_len - off &&
-                              !(fl & (kFlagRejected | VPCSUM_F_RAW)) && dv.z == u_z && kd == u_kd && rel <= u_rel63;
+                              !(fl & (kFlagRejected | VPCSUM_F_RAW)) && dv.z == u_z && kd == u_kd;
             if (__ballot(cand) == ~0ull) {
                 const int u_len = (int)(u_z & 0xffff), u_l4o = (int)(u_z >> 16);
                 const int u_ver = (int)(u_kd & 0xff), u_r0 = (int)(u_kd >> 24);
                 const DescRules ur = desc_rules(u_len, u_l4o, u_ver, (int)((u_kd >> 8) & 0xff), (int)((u_kd >> 16) & 0xff));
-                const uint32_t hiw = u_rel63 + (uint32_t)((u_r0 + u_len + 15) & ~15);   // bytes of the window
+                const int nchw = (u_r0 + u_len + 15) >> 4;                     // chunks per packet
+                const uint32_t hiw = u_rel63 + 16u * (uint32_t)nchw;           // bytes of the window
+                // contiguous: lane 63 last, all within 4 KB of lane 0's first chunk; otherwise
+                // (any frame layout, e.g. 2-KB umem frames) gathered, for packets of <= 4 chunks
+                const bool contig = __ballot(rel <= u_rel63) == ~0ull && hiw <= 4096u;
                 if (!ur.bad && !(u_r0 & 1) && u_len <= 64 && ((u_ver == 4 && u_l4o == 20) || (u_ver == 6 && u_l4o == 40)) &&
-                    hiw <= 4096u) {
+                    (contig || nchw <= 4)) {
                     fastu = true;
                     bad = false;
                     do_ip = ur.do_ip;
@@ -708,7 +712,8 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                     // the large tier's phase B (+20 VGPRs, one wave per SIMD less)
                     uint32_t ln = (uint32_t)lane;
                     asm volatile("" : "+v"(ln));
-                    {
+                    uint32_t c0;   // this lane's first chunk in the LDS window
+                    if (contig) {
                         v4u c[4];
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
@@ -717,12 +722,28 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                         }
 #pragma unroll
                         for (int u = 0; u < 4; ++u) win[win_slot(64u * u + ln)] = c[u];
+                        c0 = rel >> 4;
+                    } else {
+                        // gathered: flat chunk f = 64u + lane is chunk f % nchw of packet f / nchw,
+                        // whose first chunk comes from that packet's lane
+                        const uint32_t mul = nchw == 1 ? 65536u : nchw == 2 ? 32768u : nchw == 3 ? 21846u : 16384u;
+                        v4u c[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint32_t f = 64u * u + ln;
+                            const uint32_t pk = (f * mul) >> 16;
+                            const uint32_t src = (uint32_t)__shfl((int)boff, (int)(pk & 63u), 64);
+                            c[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                                rsrc, u < nchw ? src + ((f - pk * (uint32_t)nchw) << 4) : kOutOfRange, 0, NT ? 2 : 0);
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (u < nchw) win[win_slot(64u * u + ln)] = c[u];
+                        c0 = ln * (uint32_t)nchw;
                     }
                     wave_sync_lds();
                     // this lane's chunks [c0, c0 + 5): 20 dwords from its chunk-aligned start
                     uint32_t x[20];
-                    const uint32_t c0 = rel >> 4;
-                    const int nchw = (u_r0 + u_len + 15) >> 4;
 #pragma unroll
                     for (int k = 0; k < 5; ++k) {
                         v4u v = v4u{0, 0, 0, 0};
