@@ -392,7 +392,7 @@ def main():
     traffic, traffic_src = pmc_traffic("nat" if nat else args.workload) if args.team == 0 else (None, None)
     if rank == 0:
         value = total_bytes_step * args.steps / wall_max / 1e9
-        kname = "k_nat4w (RFC 1624)" if nat else "k_csum_d (K2)"
+        kname = "k_natw (RFC 1624)" if nat else "k_csum_d (K2)"
         line = {
             "metric": METRIC,
             "value": round(value, 2),
