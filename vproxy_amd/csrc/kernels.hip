@@ -385,12 +385,18 @@ __device__ __forceinline__ void wave_sync_lds() {
     asm volatile("" ::: "memory");
 }
 
+// acc + both 16-bit halves of w, one v_sad_u16 (|w.hi - 0| + |w.lo - 0| + acc).  A sum of
+// halfwords folds to the same one's-complement value as the sum of the dwords they form (equal
+// mod 0xffff, zero only for zero data) and needs no carry chain: one VALU op per dword instead
+// of a 64-bit add's two, and one accumulator register instead of two.
+__device__ __forceinline__ uint32_t hsum(uint32_t acc, uint32_t w) { return __builtin_amdgcn_sad_u16(w, 0u, acc); }
+
 // Fast-class trips of one team over its packet's chunks [0, nch): U loads per lane issued
 // back to back, then consumed (payload fast path, masked tail, header bitmaps).
 template <int TEAM, int U, bool VERIFY, bool NT>
 __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, uint32_t boff, int nch, int klo,
-                                           uint32_t kfast, int l4hi, const uint4 bm, int tl, uint64_t& acc_l4,
-                                           uint64_t& acc_ip, uint32_t& st_ip, uint32_t& st_l4) {
+                                           uint32_t kfast, int l4hi, const uint4 bm, int tl, uint32_t& acc_l4,
+                                           uint32_t& acc_ip, uint32_t& st_ip, uint32_t& st_l4) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     for (int rr = 0; rr * TEAM < nch; rr += U) {
         v4u v[U];
@@ -404,21 +410,20 @@ __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, ui
         for (int u = 0; u < U; ++u) {
             const int k = (rr + u) * TEAM + tl;
             if ((uint32_t)(k - klo) < kfast) {
-                acc_l4 += (uint64_t)v[u].x + v[u].y;
-                acc_l4 += (uint64_t)v[u].z + v[u].w;
+                acc_l4 = hsum(hsum(hsum(hsum(acc_l4, v[u].x), v[u].y), v[u].z), v[u].w);
             } else if (k >= klo) {
                 const int c = k << 4;
                 const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
+                for (int j = 0; j < 4; ++j) acc_l4 = hsum(acc_l4, w[j] & tailmask(c + 4 * j, l4hi));
             } else if (u * TEAM < 4) {   // header chunks: k < klo <= 4
                 const int hb0 = k << 3;
                 const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int hb = hb0 + 2 * j;
-                    acc_ip += w[j] & hmask((bm.x >> hb) & 3);
-                    acc_l4 += w[j] & hmask((bm.y >> hb) & 3);
+                    acc_ip = hsum(acc_ip, w[j] & hmask((bm.x >> hb) & 3));
+                    acc_l4 = hsum(acc_l4, w[j] & hmask((bm.y >> hb) & 3));
                     if (VERIFY) {
                         st_ip += w[j] & hmask((bm.z >> hb) & 3);
                         st_l4 += w[j] & hmask((bm.w >> hb) & 3);
@@ -466,9 +471,10 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
         const int l4hi = (int)a.w;
         uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
         uint32_t st_ip = 0, st_l4 = 0;
+        uint32_t h_l4 = 0, h_ip = 0;   // fast class: halfword sums
         if (a.y >> 31) {
             const uint4 bm = sl[1];
-            fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, acc_l4, acc_ip, st_ip, st_l4);
+            fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip, st_ip, st_l4);
         } else if (nch > 0) {
             const uint4 q2 = sl[2], q3 = sl[3];
             PktPlan pl;
@@ -496,8 +502,8 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
                 asm volatile("" ::"v"(vv.x), "v"(vv.y), "v"(vv.z), "v"(vv.w));
             }
         }
-        const uint32_t s_l4 = fold32(team_sum<TEAM>(fold64(acc_l4)));
-        const uint32_t s_ip = fold32(team_sum<TEAM>(fold64(acc_ip)));
+        const uint32_t s_l4 = fold32(team_sum<TEAM>(fold64(acc_l4 + h_l4)));
+        const uint32_t s_ip = fold32(team_sum<TEAM>(fold64(acc_ip + h_ip)));
         const uint32_t s_ps = fold32(team_sum<TEAM>(fold64(acc_ps)));
         uint32_t s_st = 0;
         if (VERIFY) s_st = fold32(team_sum<TEAM>(fold32(st_l4))) | (fold32(team_sum<TEAM>(fold32(st_ip))) << 16);
@@ -559,10 +565,10 @@ __device__ __forceinline__ uint4 win_sums(const uint32_t (&x)[20], int sh, int v
     const int l4d = ver == 4 ? 5 : 10;
     const int nd = (len + 3) >> 2;
     const uint32_t tail = (len & 3) ? (0xffffffffu >> (8 * (4 - (len & 3)))) : 0xffffffffu;
-    uint64_t ip = 0, l4 = 0;
+    uint32_t ip = 0, l4 = 0;   // halfword sums (hsum)
     uint32_t st_ip = 0, st_l4 = 0;
     if (do_ip) {   // IPv4 only (checked with the descriptor)
-        ip = (uint64_t)a[0] + a[1] + (a[2] & 0xffffu) + a[3] + a[4];
+        ip = hsum(hsum(hsum(hsum(hsum(0u, a[0]), a[1]), a[2] & 0xffffu), a[3]), a[4]);
         st_ip = a[2] >> 16;
     }
     if (do_l4) {
@@ -570,8 +576,11 @@ __device__ __forceinline__ uint4 win_sums(const uint32_t (&x)[20], int sh, int v
         const int fd = fo >> 2;
         const uint32_t fkeep = (fo & 2) ? 0x0000ffffu : 0xffff0000u;
         if (proto != 1) {
-            if (ver == 4) l4 = (uint64_t)a[3] + a[4];
-            else l4 = (uint64_t)a[2] + a[3] + a[4] + a[5] + a[6] + a[7] + a[8] + a[9];
+            if (ver == 4) l4 = hsum(hsum(0u, a[3]), a[4]);
+            else {
+#pragma unroll
+                for (int k = 2; k < 10; ++k) l4 = hsum(l4, a[k]);
+            }
         }
 #pragma unroll
         for (int k = 5; k < 16; ++k) {
@@ -582,11 +591,11 @@ __device__ __forceinline__ uint4 win_sums(const uint32_t (&x)[20], int sh, int v
                     st_l4 = (fo & 2) ? w >> 16 : w & 0xffffu;
                     w &= fkeep;
                 }
-                if (!psonly) l4 += w;
+                if (!psonly) l4 = hsum(l4, w);
             }
         }
     }
-    return make_uint4(fold32(fold64(l4)), fold32(fold64(ip)), 0u, VERIFY ? (st_l4 | (st_ip << 16)) : 0u);
+    return make_uint4(fold32(l4), fold32(ip), 0u, VERIFY ? (st_l4 | (st_ip << 16)) : 0u);
 }
 
 // K2 body for workgroup `blk` of a grid of `gdim` workgroups (k_csum_d: the launch grid;
