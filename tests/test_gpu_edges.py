@@ -70,7 +70,7 @@ def _assert_pins(packets, out):
             assert int(o) & 0xFFFF == p["want_ip"], p["kind"]
 
 
-TEAMS = [0, 2, 3, 6, 9, 12, 40, 45, 46, 47, 50, 62, 66, 70]
+TEAMS = [0, 2, 3, 6, 9, 12, 40, 45, 46, 47, 50, 62, 66, 70, 74]
 
 
 @pytest.mark.parametrize("pad", [0, 1, 14])

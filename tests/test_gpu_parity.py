@@ -72,7 +72,7 @@ def pack(frames, infos, stride=None, pad=0):
 
 
 @pytest.mark.parametrize("pad", [0, 1, 2, 3, 14, 15, 398])
-@pytest.mark.parametrize("team", [0, 2, 3, 5, 6, 9, 12, 40, 41, 43, 45, 46, 47, 48, 49, 50, 54, 58, 62, 66, 70])
+@pytest.mark.parametrize("team", [0, 2, 3, 5, 6, 9, 12, 40, 41, 43, 45, 46, 47, 48, 49, 50, 54, 58, 62, 66, 70, 74])
 def test_kats_on_gpu(V, orc, pad, team):
     kats, frames, infos = kat_batch()
     arena, desc = pack(frames, infos, pad=pad)
@@ -129,7 +129,7 @@ def test_synth_matches_oracle_and_checksums(V, orc, workload, pad):
     torch.cuda.synchronize()
     assert np.array_equal(arena.cpu().numpy(), arena_o), "GPU generator differs from oracle generator"
     assert np.array_equal(V.tensor_to_desc(d), desc_o)
-    for team in (0, 2, 6, 9, 12, 40, 41, 43, 45, 46, 47, 48, 49, 50, 62, 66, 70):
+    for team in (0, 2, 6, 9, 12, 40, 41, 43, 45, 46, 47, 48, 49, 50, 62, 66, 70, 74):
         out, st, written = gpu_compute(V, arena_o, desc_o, O.MODE_COMPUTE, team, write=True)
         a2 = arena_o.copy()
         oout, ost = orc.process(a2, desc_o, O.MODE_COMPUTE, write=True)
@@ -183,7 +183,7 @@ def test_bad_descriptors(V, orc, team):
     assert np.array_equal(after, arena)
 
 
-@pytest.mark.parametrize("team", [0, 8, 40, 41, 45, 46, 47, 48, 62, 66, 70])
+@pytest.mark.parametrize("team", [0, 8, 40, 41, 45, 46, 47, 48, 62, 66, 70, 74])
 @pytest.mark.parametrize("mode", [O.MODE_COMPUTE, O.MODE_VERIFY])
 def test_mixed_batch_bad_raw_interleaved(V, orc, team, mode):
     """Rejected, raw-range and slow-class (odd offset) descriptors interleaved with ordinary

@@ -435,20 +435,79 @@ __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, ui
     }
 }
 
+// One team of TEAM lanes streams the packet of slot sidx (act: the team has one) and leaves its
+// {l4, ip, pseudo, stored} sums in the slot's q0.
+template <int TEAM, int U, bool VERIFY, bool NT>
+__device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uint4 (*slots)[4], int tl, int sidx,
+                                          bool act) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    uint4* sl = slots[act ? sidx : 0];
+    uint4 a = sl[0];
+    if (!act) a = make_uint4(0, 0, 0, 0);
+    const uint32_t boff = a.x;
+    const int nch = (int)(a.y & 0xffff);
+    const int klo = (int)((a.y >> 16) & 0x3fff);
+    const uint32_t kfast = a.z;
+    const int l4hi = (int)a.w;
+    uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
+    uint32_t st_ip = 0, st_l4 = 0;
+    uint32_t h_l4 = 0, h_ip = 0;   // fast class: halfword sums
+    if (a.y >> 31) {
+        const uint4 bm = sl[1];
+        fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip, st_ip, st_l4);
+    } else if (nch > 0) {
+        const uint4 q2 = sl[2], q3 = sl[3];
+        PktPlan pl;
+        pl.r0 = (int)q2.x; pl.l4lo = (int)q2.y; pl.fa = (int)q2.z; pl.iphi = (int)q2.w;
+        pl.iplo = (int)q3.x; pl.pslo = (int)q3.y; pl.pshi = (int)q3.z;
+        pl.l4hi = l4hi; pl.nch = nch;
+        const bool dip = (a.y >> 30) & 1;
+        for (int r = 0; r * TEAM < nch; ++r) {
+            const int k = r * TEAM + tl;
+            const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
+            const v4u vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
+            const int c = k << 4;
+            const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+            if ((uint32_t)(k - klo) < kfast) {
+                acc_l4 += (uint64_t)w[0] + w[1];
+                acc_l4 += (uint64_t)w[2] + w[3];
+            } else if (k >= klo) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    hdr_dword(w[j], c + 4 * j, pl, dip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
+            }
+            asm volatile("" ::"v"(vv.x), "v"(vv.y), "v"(vv.z), "v"(vv.w));
+        }
+    }
+    const uint32_t s_l4 = fold32(team_sum<TEAM>(fold64(acc_l4 + h_l4)));
+    const uint32_t s_ip = fold32(team_sum<TEAM>(fold64(acc_ip + h_ip)));
+    const uint32_t s_ps = fold32(team_sum<TEAM>(fold64(acc_ps)));
+    uint32_t s_st = 0;
+    if (VERIFY) s_st = fold32(team_sum<TEAM>(fold32(st_l4))) | (fold32(team_sum<TEAM>(fold32(st_ip))) << 16);
+    if (act && tl == 0) sl[0] = make_uint4(s_l4, s_ip, s_ps, s_st);
+}
+
 // Phase B of K2 for one tier: slots [s_begin, s_end) streamed by teams of TEAM lanes, 64/TEAM
-// packets per iteration; each team leaves {l4, ip, pseudo, stored} sums in its slot's q0.
-template <int TEAM, int U, bool VERIFY, bool NT, bool SLOTROT = false>
+// packets per iteration.  WT: a last iteration that fills at most half of its teams (the tail of
+// the tier's costliest class, in a size-sorted unit) runs with teams of 2 x TEAM lanes, so its
+// packets need half the trips.
+template <int TEAM, int U, bool VERIFY, bool NT, bool SLOTROT = false, bool WT = false>
 __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, uint4 (*slots)[4], int lane,
                                             int s_begin, int s_end, uint32_t rot = 0) {
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     constexpr int PPI = 64 / TEAM;
     const int tl = lane & (TEAM - 1);
     const int tid = lane / TEAM;
     // rot: this wave starts at iteration rot (mod the count), so that waves whose units are a
     // power-of-two stride apart do not read the same offsets within their units at once
-    const int nit = (s_end - s_begin + PPI - 1) / PPI;
     const int range = s_end - s_begin;
+    int nit = (range + PPI - 1) / PPI;
     const int r0 = nit > 0 ? (int)(rot % (uint32_t)(SLOTROT ? range : nit)) : 0;
+    const int rem = range % PPI;
+    const bool wide = WT && TEAM <= 16 && rot == 0 && rem > 0 && 2 * rem <= PPI;
+    if (wide) --nit;
 #pragma unroll 1
     for (int it = 0; it < nit; ++it) {
         int sidx;
@@ -461,53 +520,12 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
             sidx = s_begin + (it + r0 < nit ? it + r0 : it + r0 - nit) * PPI + tid;
             act = sidx < s_end;
         }
-        uint4* sl = slots[act ? sidx : 0];
-        uint4 a = sl[0];
-        if (!act) a = make_uint4(0, 0, 0, 0);
-        const uint32_t boff = a.x;
-        const int nch = (int)(a.y & 0xffff);
-        const int klo = (int)((a.y >> 16) & 0x3fff);
-        const uint32_t kfast = a.z;
-        const int l4hi = (int)a.w;
-        uint64_t acc_l4 = 0, acc_ip = 0, acc_ps = 0;
-        uint32_t st_ip = 0, st_l4 = 0;
-        uint32_t h_l4 = 0, h_ip = 0;   // fast class: halfword sums
-        if (a.y >> 31) {
-            const uint4 bm = sl[1];
-            fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip, st_ip, st_l4);
-        } else if (nch > 0) {
-            const uint4 q2 = sl[2], q3 = sl[3];
-            PktPlan pl;
-            pl.r0 = (int)q2.x; pl.l4lo = (int)q2.y; pl.fa = (int)q2.z; pl.iphi = (int)q2.w;
-            pl.iplo = (int)q3.x; pl.pslo = (int)q3.y; pl.pshi = (int)q3.z;
-            pl.l4hi = l4hi; pl.nch = nch;
-            const bool dip = (a.y >> 30) & 1;
-            for (int r = 0; r * TEAM < nch; ++r) {
-                const int k = r * TEAM + tl;
-                const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
-                const v4u vv = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
-                const int c = k << 4;
-                const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-                if ((uint32_t)(k - klo) < kfast) {
-                    acc_l4 += (uint64_t)w[0] + w[1];
-                    acc_l4 += (uint64_t)w[2] + w[3];
-                } else if (k >= klo) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc_l4 += w[j] & tailmask(c + 4 * j, l4hi);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        hdr_dword(w[j], c + 4 * j, pl, dip, acc_l4, acc_ip, acc_ps, st_l4, st_ip, VERIFY);
-                }
-                asm volatile("" ::"v"(vv.x), "v"(vv.y), "v"(vv.z), "v"(vv.w));
-            }
-        }
-        const uint32_t s_l4 = fold32(team_sum<TEAM>(fold64(acc_l4 + h_l4)));
-        const uint32_t s_ip = fold32(team_sum<TEAM>(fold64(acc_ip + h_ip)));
-        const uint32_t s_ps = fold32(team_sum<TEAM>(fold64(acc_ps)));
-        uint32_t s_st = 0;
-        if (VERIFY) s_st = fold32(team_sum<TEAM>(fold32(st_l4))) | (fold32(team_sum<TEAM>(fold32(st_ip))) << 16);
-        if (act && tl == 0) sl[0] = make_uint4(s_l4, s_ip, s_ps, s_st);
+        tier_team<TEAM, U, VERIFY, NT>(rsrc, slots, tl, sidx, act);
+    }
+    if (WT && TEAM <= 16 && wide) {
+        constexpr int T2 = TEAM <= 16 ? 2 * TEAM : TEAM;
+        const int sidx = s_begin + nit * PPI + lane / T2;
+        tier_team<T2, U, VERIFY, NT>(rsrc, slots, lane & (T2 - 1), sidx, sidx < s_end);
     }
 }
 
@@ -602,7 +620,7 @@ __device__ __forceinline__ uint4 win_sums(const uint32_t (&x)[20], int sh, int v
 // k_csum_service: the persistent service grid, once per batch).
 // ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
 // ROT > 0 rotates whole iterations (64 / TEAM packets), ROT < 0 single slots.
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false>
 __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -913,7 +931,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         // ---- phase B: teams stream the packets in slot order ----
         if (TS > 0) {
             stream_tier<(TS > 0 ? TS : 1), US, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, n_small);
-            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0)>(rsrc, s_slot[wid], lane, n_small, 64,
+            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0), WT>(rsrc, s_slot[wid], lane, n_small, 64,
                                              // rotated only when the tier is one cost class: in a
                                              // sorted mixed tier the wrap would pair unlike sizes
                                              (ROT && n_cls == 1) ? (blk * 4u + (uint32_t)wid) * (uint32_t)(ROT < 0 ? -ROT : ROT) : 0u);
@@ -932,13 +950,13 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     }
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
                                                 uint8_t* __restrict__ arena_w, uint32_t low_grid) {
-    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF>(arena, arena_len, desc, n, out, status, flags_override, arena_w,
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT>(arena, arena_len, desc, n, out, status, flags_override, arena_w,
                                                 low_grid, blockIdx.x, gridDim.x);
 }
 
@@ -1155,7 +1173,7 @@ static uint32_t default_low_grid() {
     return (uint32_t)num_cus(dev) * 2u;
 }
 
-template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, bool adapt, hipStream_t stream) {
@@ -1176,7 +1194,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
+    hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
                        (const uint4*)desc, n, out, status, flags_override, arena_w, low_grid)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -1229,6 +1247,7 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 66: return launch_d<8, 6, 2, 2, 1, 0, 1>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         // 70: the default; 72: the default without window units (A/B)
         case 72: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 74: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 70:
         case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         default: return hipErrorInvalidValue;   // unknown kernel variant id
