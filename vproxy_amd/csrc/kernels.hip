@@ -637,7 +637,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     // waves of a workgroup interleave in groups of 8 over 256 consecutive packets, so the teams
     // of the whole workgroup read one contiguous 64-KB window per iteration (one DRAM stream
     // per workgroup instead of four).
-    const uint32_t lo = IL ? (uint32_t)((lane >> 3) * 32 + wid * 8 + (lane & 7)) : (uint32_t)lane;
+    const uint32_t lo = IL == 1 ? (uint32_t)((lane >> 3) * 32 + wid * 8 + (lane & 7)) : (uint32_t)lane;
     // Concurrency by packet size (low_grid > 0).  Large uniform packets stream fastest with few
     // packets in flight (2 workgroups per CU), small and mixed ones need the full grid to hide
     // per-iteration latency.  Every wave reads the same 64 descriptors,
@@ -648,7 +648,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     // Workgroups below low_grid work in either case and fetch their first descriptors before
     // the sample, so the two loads overlap.
     uint32_t grid = gdim;
-    uint32_t P0 = IL ? blk * 256u : ((blk * 256u + threadIdx.x) >> 6) * 64u;
+    uint32_t P0 = IL == 1 ? blk * 256u : ((blk * 256u + threadIdx.x) >> 6) * 64u;
     uint4 dnext = make_uint4(0, 0, 0, 0);
     int fnext = 0;
     const bool sample = low_grid != 0 && grid > low_grid;
@@ -1186,11 +1186,11 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     // and only when the arena is large enough to hold n packets of >= 1 KiB without overlap
     // (otherwise the sample cannot succeed and its load latency would be pure cost)
     const uint32_t low_grid =
-        (grid > 0 || IL != 0 || !adapt || arena_len < (uint64_t)n * 1024u) ? 0u : default_low_grid();
+        (grid > 0 || IL == 1 || !adapt || arena_len < (uint64_t)n * 1024u) ? 0u : default_low_grid();
     // Dense small frames (at most 128 arena bytes per packet): 5 workgroups per CU, all resident,
     // beat the 12 of the grid-stride default (C1 window units: 4.64 vs 4.49 TB/s, DESIGN.md §5
     // item 16); the arena size alone tells, no sample needed.
-    if (grid <= 0 && adapt && IL == 0 && arena_len <= (uint64_t)n * 128u) g = min(g, default_dense_grid());
+    if (grid <= 0 && adapt && IL != 1 && arena_len <= (uint64_t)n * 128u) g = min(g, default_dense_grid());
     if (g > need) g = need;
     if (g == 0) g = 1;
 #define VPC_LAUNCH(V, N)                                                                                         \
