@@ -783,6 +783,48 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                     else if (q == 1) fsums = win_sums<1, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
                     else if (q == 2) fsums = win_sums<2, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
                     else fsums = win_sums<3, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
+                    // phase C of a window unit, on the unit's (scalar) descriptor values: the
+                    // same arithmetic as finish() below, without its per-lane branches
+                    {
+                        const int u_l4o2 = u_l4o, u_r02 = u_r0;
+                        uint32_t l4c = 0, ipc = 0;
+                        if (ur.do_l4) {
+                            uint32_t tot = orient(fsums.x, u_r02 + u_l4o2);
+                            if (u_proto != 1) {
+                                const uint32_t l4len = (uint32_t)(u_len - u_l4o2);
+                                tot += orient(fsums.z, u_r02) + (uint32_t)u_proto + (l4len & 0xffff) + (l4len >> 16);
+                            }
+                            if (ur.psonly) l4c = fold32(tot);
+                            else {
+                                l4c = 0xffff - fold32(tot);
+                                if (u_proto == 17 && l4c == 0) l4c = 0xffff;
+                            }
+                        }
+                        if (ur.do_ip) ipc = 0xffff - orient(fsums.y, u_r02);
+                        uint32_t st = VPCSUM_S_DONE;
+                        if (VERIFY) {
+                            if (ur.do_ip && orient(fsums.w >> 16, u_r02) == ipc) st |= VPCSUM_S_IP_OK;
+                            if (ur.do_l4) {
+                                const uint32_t stored = orient(fsums.w & 0xffff, u_r02 + u_l4o2 + ur.fld);
+                                if (stored == l4c) st |= VPCSUM_S_L4_OK;
+                                if (!ur.psonly && u_proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
+                            }
+                        }
+                        asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
+                        if (arena_w) {
+                            uint8_t* w = arena_w + off;
+                            if (ur.do_ip) st_be16_nt(w + 10, ipc);
+                            if (ur.do_l4) st_be16_nt(w + u_l4o2 + ur.fld, l4c);
+                        }
+                        const uint32_t res_out = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
+                        if (NT) {
+                            if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lo));
+                            if (status) __builtin_nontemporal_store((uint8_t)st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lo));
+                        } else {
+                            if (out) out[P0 + lo] = res_out;
+                            if (status) status[P0 + lo] = (uint8_t)st;
+                        }
+                    }
                 }
             }
         }
@@ -923,8 +965,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
 
         uint4 sums;
         if (fastu) {
-            asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
-            sums = fsums;
+            sums = fsums;   // finished above
         } else {
         wave_sync_lds();
 
@@ -945,7 +986,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
         sums = s_slot[wid][key][0];
         }
-        finish(sums);
+        if (!fastu) finish(sums);
         wave_sync_lds();   // slots are rewritten by the next super-iteration
     }
 }
