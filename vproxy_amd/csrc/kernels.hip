@@ -1202,10 +1202,12 @@ static uint32_t default_grid() {
     return (uint32_t)num_cus(dev) * 12u;
 }
 // Grid of K2 for dense small frames: 5 workgroups per CU (all resident at 5 waves per SIMD).
-static uint32_t default_dense_grid() {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    return (uint32_t)num_cus(dev) * 5u;
+// Workgroups of one K2 build resident per CU (its VGPR and LDS use: 6 for the compute build at
+// 79 VGPRs, 5 for the verify build at 95), looked up once per build.
+static uint32_t resident_wgs(const void* kern) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, 0) != hipSuccess || nb <= 0) nb = 5;
+    return (uint32_t)nb;
 }
 // Low-concurrency grid of K2 for batches of large packets: 2 workgroups per CU.
 static uint32_t default_low_grid() {
@@ -1228,15 +1230,26 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     // (otherwise the sample cannot succeed and its load latency would be pure cost)
     const uint32_t low_grid =
         (grid > 0 || IL == 1 || !adapt || arena_len < (uint64_t)n * 1024u) ? 0u : default_low_grid();
-    // Dense small frames (at most 128 arena bytes per packet): 5 workgroups per CU, all resident,
-    // beat the 12 of the grid-stride default (C1 window units: 4.64 vs 4.49 TB/s, DESIGN.md §5
-    // item 16); the arena size alone tells, no sample needed.
-    if (grid <= 0 && adapt && IL != 1 && arena_len <= (uint64_t)n * 128u) g = min(g, default_dense_grid());
-    if (g > need) g = need;
-    if (g == 0) g = 1;
+    // Dense small frames (at most 128 arena bytes per packet): one resident round of workgroups
+    // beats the grid-stride default (C1 window units at 6 per CU: 4.91 vs 4.63 TB/s at 5 and
+    // 4.65 at 12); the arena size alone tells, no sample needed.
+    const bool dense = grid <= 0 && adapt && IL != 1 && arena_len <= (uint64_t)n * 128u;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint32_t cus = (uint32_t)num_cus(dev);
 #define VPC_LAUNCH(V, N)                                                                                         \
-    hipLaunchKernelGGL((k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT>), dim3(g), dim3(256), 0, stream, arena, arena_len,                 \
-                       (const uint4*)desc, n, out, status, flags_override, arena_w, low_grid)
+    do {                                                                                                         \
+        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT>;                                       \
+        uint32_t gg = g;                                                                                         \
+        if (dense) {                                                                                             \
+            static const uint32_t res = resident_wgs((const void*)kern);                                         \
+            gg = min(gg, res * cus);                                                                             \
+        }                                                                                                        \
+        if (gg > need) gg = need;                                                                                \
+        if (gg == 0) gg = 1;                                                                                     \
+        hipLaunchKernelGGL(kern, dim3(gg), dim3(256), 0, stream, arena, arena_len, (const uint4*)desc, n, out,   \
+                           status, flags_override, arena_w, low_grid);                                            \
+    } while (0)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
     } else {
