@@ -1,0 +1,61 @@
+"""A/B of kernel variants on data the caches cannot hold between launches (tooling).
+
+The bench re-reads one resident batch, so lines a kernel leaves in the 256-MB Infinity Cache can
+serve the next launch.  Here NB batches of the workload lie in NB arenas, and the launches rotate
+over them: the lines touched per round exceed the cache, so each launch reads its batch from HBM.
+Prints algorithmic GB/s per variant, rotating and (for comparison) repeating one batch.
+usage: python tools/cold_ab.py --workload c1 --stride 2048 --teams 70,73 [--batches 4]"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vproxy_amd import vpcsum as V  # noqa: E402
+from bench import WORKLOADS, algorithmic_bytes  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="c1")
+ap.add_argument("--stride", type=int, default=0)
+ap.add_argument("--teams", default="70,73")
+ap.add_argument("--batches", type=int, default=4)
+ap.add_argument("--rounds", type=int, default=4)
+ap.add_argument("--iters", type=int, default=40)
+args = ap.parse_args()
+
+sid, n, stride, text = WORKLOADS[args.workload]
+stride = args.stride or stride
+nb = args.batches
+# one arena per batch (each below 4 GiB, as K2's buffer addressing needs), disjoint sub-streams
+arenas = [torch.zeros(n * stride, dtype=torch.uint8, device="cuda") for _ in range(nb)]
+descs = [torch.zeros(n * 16, dtype=torch.uint8, device="cuda") for _ in range(nb)]
+for b in range(nb):
+    V.synth(arenas[b], n, stride, 0, sid, 0x20241020, b * n, descs[b])
+torch.cuda.synchronize()
+nbytes = algorithmic_bytes(V.tensor_to_desc(descs[0]))
+out = torch.zeros(n, dtype=torch.int32, device="cuda")
+ref = torch.zeros(n, dtype=torch.int32, device="cuda")
+variants = [int(t) for t in args.teams.split(",")]
+V.compute(arenas[1], descs[1], n, ref, None, 0, 4)
+for t in variants:   # every variant's results, once
+    V.compute(arenas[1], descs[1], n, out, None, 0, t)
+    assert torch.equal(out, ref), f"variant {t} differs"
+res = {(t, m): [] for t in variants for m in ("rotate", "repeat")}
+e0, e1 = V.Event(), V.Event()
+for r in range(args.rounds):
+    for t in variants:
+        for m in ("rotate", "repeat"):
+            pick = (lambda i: i % nb) if m == "rotate" else (lambda i: 0)
+            for i in range(nb):
+                V.compute(arenas[pick(i)], descs[pick(i)], n, out, None, 0, t)
+            e0.record()
+            for i in range(args.iters):
+                V.compute(arenas[pick(i)], descs[pick(i)], n, out, None, 0, t)
+            e1.record()
+            torch.cuda.synchronize()
+            res[(t, m)].append(nbytes / (e0.elapsed_ms(e1) / args.iters) / 1e6)
+print(f"{text}, stride {stride}, {nb} batches of {n} packets: algorithmic {nbytes / n:.1f} B/pkt")
+for (t, m), a in res.items():
+    print(f"variant={t} {m:6s}: median {np.median(a):7.1f} GB/s  max {max(a):7.1f}")

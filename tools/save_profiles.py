@@ -30,10 +30,10 @@ def json_line(log):
 
 
 def summarise(src, dst, kern, packets):
-    """Mean of each counter over the kernel's dispatches, plus HBM bytes per launch.  Reads: the
-    guide's gfx950 rule for wide streaming reads (FETCH_SIZE counts half: x2); the NAT kernel's
-    reads are scattered 16-48 B header windows, for which the rule is not established, so both
-    the raw and the doubled figure are kept (NAT)."""
+    """Mean of each counter over the kernel's dispatches, plus HBM bytes per launch.  Reads:
+    FETCH_SIZE = TCC_EA0_RDREQ x 64 B, and every read request of these kernels is 128 B
+    (TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ for K2 on C1-C3 and for the NAT kernel's scattered header
+    windows, profiles/r02u_read_request_sizes.json): read bytes = 2 x FETCH_SIZE for both."""
     vals = {}
     os.makedirs(dst, exist_ok=True)
     for f in sorted(glob.glob(os.path.join(src, "p*_counter_collection.csv"))):
@@ -52,23 +52,29 @@ def summarise(src, dst, kern, packets):
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         rd, wr = mean["FETCH_SIZE"] * 1024, mean["WRITE_SIZE"] * 1024
         out["write_bytes"] = wr
-        if kern == "k_csum":
-            out["read_bytes_corrected"] = 2 * rd
-            out["hbm_bytes_per_launch"] = 2 * rd + wr
-            out["correction"] = "read = 2 x FETCH_SIZE (gfx950 half-count of 128-B streaming requests), MI355X_MICROARCH.md §HBM"
-        else:
-            out["read_bytes_raw"] = rd
-            out["read_bytes_doubled"] = 2 * rd
-            out["hbm_bytes_per_launch"] = rd + wr
-            out["hbm_bytes_per_launch_doubled_reads"] = 2 * rd + wr
-            out["correction"] = ("scattered header windows: FETCH_SIZE taken as is (one 64-B request per "
-                                 "window); the doubled figure is the streaming rule, an upper bound")
+        out["read_bytes_corrected"] = 2 * rd
+        out["hbm_bytes_per_launch"] = 2 * rd + wr
+        out["correction"] = ("read = 2 x FETCH_SIZE: FETCH_SIZE tallies 64 B per request and every read "
+                             "request is 128 B (TCC_EA0_RDREQ_128B, profiles/r02u_read_request_sizes.json)")
         for k in ("hbm_bytes_per_launch", "write_bytes"):
             out[k + "_per_packet"] = round(out[k] / packets, 2)
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "TCC_EA0_RDREQ_sum", "TCC_EA0_WRREQ_sum"):
         if k in mean:
             out[k + "_per_packet"] = round(mean[k] / packets, 3)
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+
+
+def resummarise(tag):
+    """Recompute the summaries of committed PMC passes (profiles/<tag>_pmc_*/pass*.csv)."""
+    for dst in sorted(glob.glob(os.path.join(P, f"{tag}_pmc_*"))):
+        cfg = os.path.basename(dst)[len(tag) + 5:]
+        old = json.load(open(os.path.join(dst, "summary.json")))
+        tmp = dst + ".src"
+        os.makedirs(tmp, exist_ok=True)
+        for f in glob.glob(os.path.join(dst, "pass*.csv")):
+            shutil.copy(f, os.path.join(tmp, "p" + os.path.basename(f)[4:-4] + "_counter_collection.csv"))
+        summarise(tmp, dst, old["kernel_substring"], old["packets"])
+        shutil.rmtree(tmp)
 
 
 def main(tag):
@@ -94,4 +100,7 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    if sys.argv[1] == "--resummarise":
+        resummarise(sys.argv[2])
+    else:
+        main(sys.argv[1])

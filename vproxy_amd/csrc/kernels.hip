@@ -620,8 +620,7 @@ __device__ __forceinline__ uint4 win_sums(const uint32_t (&x)[20], int sh, int v
 // k_csum_service: the persistent service grid, once per batch).
 // ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
 // ROT > 0 rotates whole iterations (64 / TEAM packets), ROT < 0 single slots.
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false,
-          bool SNT = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false>
 __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -761,10 +760,8 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                             const uint32_t f = 64u * u + ln;
                             const uint32_t pk = (f * mul) >> 16;
                             const uint32_t src = (uint32_t)__shfl((int)boff, (int)(pk & 63u), 64);
-                            // temporal: sparse frames use half a line each (see the small tier)
                             c[u] = __builtin_amdgcn_raw_buffer_load_b128(
-                                rsrc, u < nchw ? src + ((f - pk * (uint32_t)nchw) << 4) : kOutOfRange, 0,
-                                (NT && SNT) ? 2 : 0);
+                                rsrc, u < nchw ? src + ((f - pk * (uint32_t)nchw) << 4) : kOutOfRange, 0, NT ? 2 : 0);
                         }
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
@@ -974,11 +971,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
 
         // ---- phase B: teams stream the packets in slot order ----
         if (TS > 0) {
-            // The small tier reads with temporal loads (SNT: non-temporal, for A/B).  Its packets use
-            // at most 64 B of a 128-B line when frames are sparse (2-KB umem frames, C3's 64-B
-            // class): a non-temporal miss fetches the whole line from HBM, a temporal one only the
-            // 64-B half it touches (C3 +3%, C1 in 2-KB frames +20%).
-            stream_tier<(TS > 0 ? TS : 1), US, VERIFY, NT && SNT>(rsrc, s_slot[wid], lane, 0, n_small);
+            stream_tier<(TS > 0 ? TS : 1), US, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, n_small);
             stream_tier<TEAM, U, VERIFY, NT, (ROT < 0), WT>(rsrc, s_slot[wid], lane, n_small, 64,
                                              // rotated only when the tier is one cost class: in a
                                              // sorted mixed tier the wrap would pair unlike sizes
@@ -998,14 +991,13 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     }
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false,
-          bool SNT = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
                                                 uint8_t* __restrict__ arena_w, uint32_t low_grid) {
-    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, SNT>(arena, arena_len, desc, n, out, status, flags_override, arena_w,
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT>(arena, arena_len, desc, n, out, status, flags_override, arena_w,
                                                 low_grid, blockIdx.x, gridDim.x);
 }
 
@@ -1224,8 +1216,7 @@ static uint32_t default_low_grid() {
     return (uint32_t)num_cus(dev) * 2u;
 }
 
-template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false,
-          bool SNT = false>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, bool adapt, hipStream_t stream) {
@@ -1248,7 +1239,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     const uint32_t cus = (uint32_t)num_cus(dev);
 #define VPC_LAUNCH(V, N)                                                                                         \
     do {                                                                                                         \
-        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT, SNT>;                                  \
+        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT>;                                       \
         uint32_t gg = g;                                                                                         \
         if (dense) {                                                                                             \
             static const uint32_t res = resident_wgs((const void*)kern);                                         \
@@ -1311,9 +1302,6 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         // 70: the default; 72: the default without window units (A/B)
         case 72: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 74: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
-        // 73 / 75: 70 / 72 with non-temporal loads in the small tier and gathered units (A/B)
-        case 73: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
-        case 75: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, false, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 70:
         case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         default: return hipErrorInvalidValue;   // unknown kernel variant id
