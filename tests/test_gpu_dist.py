@@ -27,11 +27,14 @@ def _bench(*args):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("workload", ["c2", "c3"])
+@pytest.mark.parametrize("workload", ["c2", "c3", "c1"])
 def test_bench_two_ranks_weak(workload):
+    """c1: its 64-MB batch is below the bench's 1-GiB rotation floor, so the launches rotate over
+    16 batches per rank; the gates still check batch 0."""
     j = _bench("--workload", workload)
     assert j["n_gpus"] == 2 and j["scaling"] == "weak"
     c = j["config"]
+    assert c["batches_rotated"] == (16 if workload == "c1" else 1)
     assert c["verify_all_packets"] is True
     assert c["oracle_gate"]["sample_equal"] is True
     assert c["global_batch"] == 2 * c["packets_rank0"]
