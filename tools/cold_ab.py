@@ -23,6 +23,7 @@ ap.add_argument("--teams", default="70,73")
 ap.add_argument("--batches", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--iters", type=int, default=40)
+ap.add_argument("--bpc", default="0", help="workgroups per CU to try (0 = the launcher's choice)")
 args = ap.parse_args()
 
 sid, n, stride, text = WORKLOADS[args.workload]
@@ -37,25 +38,25 @@ torch.cuda.synchronize()
 nbytes = algorithmic_bytes(V.tensor_to_desc(descs[0]))
 out = torch.zeros(n, dtype=torch.int32, device="cuda")
 ref = torch.zeros(n, dtype=torch.int32, device="cuda")
-variants = [int(t) for t in args.teams.split(",")]
+variants = [(int(t), int(b)) for t in args.teams.split(",") for b in args.bpc.split(",")]
 V.compute(arenas[1], descs[1], n, ref, None, 0, 4)
-for t in variants:   # every variant's results, once
-    V.compute(arenas[1], descs[1], n, out, None, 0, t)
+for t, b in variants:   # every variant's results, once
+    V.compute(arenas[1], descs[1], n, out, None, 0, t, blocks_per_cu=b)
     assert torch.equal(out, ref), f"variant {t} differs"
-res = {(t, m): [] for t in variants for m in ("rotate", "repeat")}
+res = {(t, b, m): [] for t, b in variants for m in ("rotate", "repeat")}
 e0, e1 = V.Event(), V.Event()
 for r in range(args.rounds):
-    for t in variants:
+    for t, b in variants:
         for m in ("rotate", "repeat"):
             pick = (lambda i: i % nb) if m == "rotate" else (lambda i: 0)
             for i in range(nb):
-                V.compute(arenas[pick(i)], descs[pick(i)], n, out, None, 0, t)
+                V.compute(arenas[pick(i)], descs[pick(i)], n, out, None, 0, t, blocks_per_cu=b)
             e0.record()
             for i in range(args.iters):
-                V.compute(arenas[pick(i)], descs[pick(i)], n, out, None, 0, t)
+                V.compute(arenas[pick(i)], descs[pick(i)], n, out, None, 0, t, blocks_per_cu=b)
             e1.record()
             torch.cuda.synchronize()
-            res[(t, m)].append(nbytes / (e0.elapsed_ms(e1) / args.iters) / 1e6)
+            res[(t, b, m)].append(nbytes / (e0.elapsed_ms(e1) / args.iters) / 1e6)
 print(f"{text}, stride {stride}, {nb} batches of {n} packets: algorithmic {nbytes / n:.1f} B/pkt")
-for (t, m), a in res.items():
-    print(f"variant={t} {m:6s}: median {np.median(a):7.1f} GB/s  max {max(a):7.1f}")
+for (t, b, m), a in res.items():
+    print(f"variant={t} bpc={b or 'def'} {m:6s}: median {np.median(a):7.1f} GB/s  max {max(a):7.1f}")
