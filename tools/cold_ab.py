@@ -23,11 +23,13 @@ ap.add_argument("--teams", default="70,73")
 ap.add_argument("--batches", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--iters", type=int, default=40)
+ap.add_argument("--packets", type=int, default=0, help="packets per batch instead of the workload's")
 ap.add_argument("--bpc", default="0", help="workgroups per CU to try (0 = the launcher's choice)")
 args = ap.parse_args()
 
 sid, n, stride, text = WORKLOADS[args.workload]
 stride = args.stride or stride
+n = args.packets or n
 nb = args.batches
 # one arena per batch (each below 4 GiB, as K2's buffer addressing needs), disjoint sub-streams
 arenas = [torch.zeros(n * stride, dtype=torch.uint8, device="cuda") for _ in range(nb)]

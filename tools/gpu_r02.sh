@@ -23,10 +23,10 @@ fi
 if has trace; then
   step trace_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline
 fi
-if has pmc; then
+if has pmc || has pmck2; then   # pmck2: the checksum configs only (PMC_CFGS, default all four)
   # FETCH_SIZE takes 3 of the 4 TCC counters and WRITE_SIZE 2: never in one pass
   P="FETCH_SIZE|WRITE_SIZE|SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES|SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES|GRBM_GUI_ACTIVE TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"
-  for w in c2 c1 c3; do
+  for w in ${PMC_CFGS:-c2 c1 c3 c4}; do
     IFS='|' read -ra PS <<< "$P"; i=0
     for c in "${PS[@]}"; do i=$((i+1)); step pmc_${w}_p$i 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_$w -o p$i -- python3 tools/prof_one.py --workload $w; done
   done
