@@ -23,6 +23,7 @@ ap.add_argument("--teams", default="70,73")
 ap.add_argument("--batches", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--iters", type=int, default=40)
+ap.add_argument("--mode", type=int, default=0, help="0 compute, 1 verify (status bytes written too)")
 ap.add_argument("--packets", type=int, default=0, help="packets per batch instead of the workload's")
 ap.add_argument("--bpc", default="0", help="workgroups per CU to try (0 = the launcher's choice)")
 args = ap.parse_args()
@@ -39,6 +40,7 @@ for b in range(nb):
 torch.cuda.synchronize()
 nbytes = algorithmic_bytes(V.tensor_to_desc(descs[0]))
 out = torch.zeros(n, dtype=torch.int32, device="cuda")
+st = torch.zeros(n, dtype=torch.uint8, device="cuda") if args.mode == 1 else None
 ref = torch.zeros(n, dtype=torch.int32, device="cuda")
 variants = [(int(t), int(b)) for t in args.teams.split(",") for b in args.bpc.split(",")]
 V.compute(arenas[1], descs[1], n, ref, None, 0, 4)
@@ -52,10 +54,10 @@ for r in range(args.rounds):
         for m in ("rotate", "repeat"):
             pick = (lambda i: i % nb) if m == "rotate" else (lambda i: 0)
             for i in range(nb):
-                V.compute(arenas[pick(i)], descs[pick(i)], n, out, None, 0, t, blocks_per_cu=b)
+                V.compute(arenas[pick(i)], descs[pick(i)], n, out, st, args.mode, t, blocks_per_cu=b)
             e0.record()
             for i in range(args.iters):
-                V.compute(arenas[pick(i)], descs[pick(i)], n, out, None, 0, t, blocks_per_cu=b)
+                V.compute(arenas[pick(i)], descs[pick(i)], n, out, st, args.mode, t, blocks_per_cu=b)
             e1.record()
             torch.cuda.synchronize()
             res[(t, b, m)].append(nbytes / (e0.elapsed_ms(e1) / args.iters) / 1e6)
