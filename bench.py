@@ -17,6 +17,10 @@ the start/stop barriers and the max-over-ranks reductions -- the data path has n
 Other workloads: c1, c3, c4 (BASELINE configs; `--workload c4 --strong` is C4's 262,144 x 9000 B
 batch sharded over the GPUs) and c5 (NAT rewrite, RFC 1624, 10M packets split over the GPUs).
 
+Uncached input: a batch smaller than 1 GiB (C1's 64-MB arena) is measured with the launches
+rotating over several batches of the same config, so that the Infinity Cache cannot serve one
+launch from the lines of the previous (`config.batches_rotated`).
+
 Correctness gate: rank 0's GPU results are compared word for word with the oracle's on the packets
 the cpu_baseline leg processes (the whole batch when its budget allows); every rank also writes its
 sums in place and verifies them (size-independent property).
