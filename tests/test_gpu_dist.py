@@ -84,3 +84,36 @@ def test_device_group_splits_by_bytes(orc, ndev, registered):
     g.wait(t1)
     assert np.array_equal(np.concatenate([o1, o2]), wout) and np.array_equal(arena, want_arena)
     g.close()
+
+
+def test_device_group_failed_submit_joins_submitted_ranges(orc):
+    """A range that a context refuses (here the second one holds more packets than a context's
+    capacity) fails the group submit only after the ranges already submitted have finished: their
+    results are in the caller's buffers when the error is returned, and the group keeps working."""
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import oracle as O
+    from vproxy_amd import vpcsum as V
+    a4, d4 = orc.synth(100, 9216, 14, O.SYNTH_C4, O.SEED, 0)       # 100 jumbo packets first
+    a1, d1 = orc.synth(3000, 128, 14, O.SYNTH_C1, O.SEED, 100)     # then 3000 small ones
+    d1 = d1.copy()
+    d1["l3_off"] += len(a4)
+    arena = np.concatenate([a4, a1])
+    d = np.concatenate([d4, d1])
+    want, _ = orc.process(arena, d, O.MODE_COMPUTE)
+    # the library's byte-balanced cut of two ranges (vpcsum_group_submit)
+    acc = np.cumsum(d["l3_len"].astype(np.int64))
+    cut = int(np.argmax(acc * 2 >= acc[-1])) + 1
+    assert cut < 1000 < len(d) - cut   # range 0 fits a context, range 1 does not
+    g = V.Group([0, 0], max_arena=arena.nbytes, max_pkts=1000)
+    out = np.zeros(len(d), np.uint32)
+    with pytest.raises(V.VpcsumError, match="capacity"):
+        g.submit(arena, d, out, None, O.MODE_COMPUTE)
+    assert np.array_equal(out[:cut], want[:cut])   # range 0 finished before the error
+    assert not out[cut:].any()
+    small = d[:cut]
+    o2, _ = g.run(arena, small, O.MODE_COMPUTE)
+    assert np.array_equal(o2, want[:cut])
+    g.close()

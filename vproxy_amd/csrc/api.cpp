@@ -1060,8 +1060,14 @@ int vpcsum_group_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len,
     for (size_t d = 0; d < k; ++d) {
         const uint32_t a = cut[d], b = std::max(cut[d], cut[d + 1]);
         if (vpcsum_ctx_submit(g->ctx[d], h_arena, arena_len, h_desc + a, b - a, h_out ? h_out + a : nullptr,
-                              h_status ? h_status + a : nullptr, mode, &slot.sub[d]) != 0)
-            return -1;
+                              h_status ? h_status + a : nullptr, mode, &slot.sub[d]) != 0) {
+            // the ranges already submitted write into the caller's buffers when they finish:
+            // join them before reporting the failure, so the caller may free its buffers
+            const std::string e = g_err;
+            for (size_t q = 0; q < d; ++q) (void)vpcsum_ctx_wait(g->ctx[q], slot.sub[q]);
+            slot.sub.clear();
+            return fail("%s", e.c_str());
+        }
     }
     slot.ticket = t;
     *ticket = t;
