@@ -935,6 +935,17 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint
             return fail("vpcsum_ctx_pipeline: descriptor %u [%llu, +%u) outside the copied frames", i,
                         (unsigned long long)off, (unsigned)h_desc[i].l3_len);
     }
+    // a failure after some chunks were queued drains both streams before it returns: the queued
+    // copies and in-place writes land in the caller's registered buffers
+#define VPC_CHECK_DRAIN(expr, what)                                                  \
+    do {                                                                             \
+        hipError_t e__ = (expr);                                                     \
+        if (e__ != hipSuccess) {                                                     \
+            const int rc__ = hipfail(e__, what);                                     \
+            for (auto& q__ : c->slots) (void)hipStreamSynchronize(q__.stream);       \
+            return rc__;                                                             \
+        }                                                                            \
+    } while (0)
     for (uint32_t k = 0; k < chunks; ++k) {
         const uint32_t i0 = k * per;
         if (i0 >= n) break;
@@ -942,18 +953,24 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint
         Slot& s = c->slots[k & 1];
         // descriptors of this chunk address the device slot as frame (i - i0) * stride: the
         // caller's descriptors are relative to frame i0 once i0 * stride is subtracted
-        VPC_CHECK(hipMemcpyAsync(s.d_desc, h_desc + i0, (size_t)m * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice,
+        VPC_CHECK_DRAIN(hipMemcpyAsync(s.d_desc, h_desc + i0, (size_t)m * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice,
                                  s.stream),
                   "pipeline H2D desc");
-        VPC_CHECK(hipMemcpy2DAsync(s.d_arena, stride, h_arena + (uint64_t)i0 * stride, stride, copy_bytes, m,
+        VPC_CHECK_DRAIN(hipMemcpy2DAsync(s.d_arena, stride, h_arena + (uint64_t)i0 * stride, stride, copy_bytes, m,
                                    hipMemcpyHostToDevice, s.stream),
                   "pipeline H2D frames");
-        VPC_CHECK(launch_csum(s.d_arena - (uint64_t)i0 * stride, (uint64_t)(i0 + m) * stride, s.d_desc, m, s.d_out,
+        VPC_CHECK_DRAIN(launch_csum(s.d_arena - (uint64_t)i0 * stride, (uint64_t)(i0 + m) * stride, s.d_desc, m, s.d_out,
                               nullptr, nullptr, mode & VPCSUM_MODE_VERIFY, w, 0, 0, s.stream),
                   "pipeline launch");
-        VPC_CHECK(hipMemcpyAsync(h_out + i0, s.d_out, (size_t)m * 4, hipMemcpyDeviceToHost, s.stream), "pipeline D2H");
+        VPC_CHECK_DRAIN(hipMemcpyAsync(h_out + i0, s.d_out, (size_t)m * 4, hipMemcpyDeviceToHost, s.stream), "pipeline D2H");
     }
-    for (auto& s : c->slots) VPC_CHECK(hipStreamSynchronize(s.stream), "pipeline sync");
+#undef VPC_CHECK_DRAIN
+    hipError_t es = hipSuccess;   // both streams are joined, the first error is reported
+    for (auto& s : c->slots) {
+        const hipError_t e2 = hipStreamSynchronize(s.stream);
+        if (es == hipSuccess) es = e2;
+    }
+    VPC_CHECK(es, "pipeline sync");
     return 0;
 }
 
