@@ -159,6 +159,32 @@ int vpcsum_parse_ether_async(const uint8_t* d_arena, uint64_t arena_len,
                              const uint64_t* d_frame_off, const uint32_t* d_frame_len, uint32_t n,
                              uint8_t flags, vpcsum_desc_t* d_desc, uint8_t* d_status, void* stream);
 
+/* Flow tuple of a parsed frame: what the vswitch's L4 input nodes read before their conntrack
+ * lookup (TcpInput.java:47-51: tcpPkt.getSrc(ipPkt) / getDst(ipPkt) -> conntrack.lookupTcp, and
+ * getFlags() == SYN -> lookupTcpListen; UdpInput.java:45-47: IPPort(ipPkt.getDst(),
+ * udpPkt.getDstPort()) -> lookupUdpListen), and what SwitchUtils.executeTcpNat / executeUdpNat
+ * compare (:321-322, :506-507).  Addresses and ports in network order; an IPv4 address is the
+ * first 4 bytes (zeros after).  Ports (TcpPacket / UdpPacket.initPartial: uint16 at 0 and 2) and
+ * tcp_flags (TcpPacket.initPartial :192-195: uint16 at 12 & 0x3f) are 0 for other protocols.  A
+ * refused frame (status S_BAD_DESC) gets an all-zero tuple (l3_ver 0). */
+typedef struct vpcsum_tuple {
+    uint8_t src[16];
+    uint8_t dst[16];
+    uint8_t sport[2];
+    uint8_t dport[2];
+    uint8_t l3_ver;      /* 4 / 6; 0: refused frame */
+    uint8_t l4_proto;
+    uint8_t tcp_flags;
+    uint8_t rsv;
+} vpcsum_tuple_t;        /* 40 bytes */
+
+/* vpcsum_parse_ether_async that also writes one vpcsum_tuple_t per frame to d_tuples (batched
+ * header parse + tuple extraction), in the same pass over the headers. */
+int vpcsum_parse_ether_tuples_async(const uint8_t* d_arena, uint64_t arena_len,
+                                    const uint64_t* d_frame_off, const uint32_t* d_frame_len, uint32_t n,
+                                    uint8_t flags, vpcsum_desc_t* d_desc, uint8_t* d_status,
+                                    vpcsum_tuple_t* d_tuples, void* stream);
+
 /* Streaming-read ceiling probe: reads `bytes` from d_buf with 16-B lanes, writes one word per
  * block into d_sink.  Used by bench.py to report a measured HBM read roof next to 8 TB/s. */
 int vpcsum_read_probe_async(const uint8_t* d_buf, uint64_t bytes, uint32_t* d_sink,

@@ -365,6 +365,33 @@ def desc_flags_for(info: L3Info, want_ip=True, want_l4=True) -> int:
     return f
 
 
+def flow_tuple(frame: bytes) -> dict:
+    """The flow tuple the L4 input nodes read before their conntrack lookup, for one Ethernet
+    frame: TcpInput.java:47-51 (tcpPkt.getSrc(ipPkt) / getDst(ipPkt) -> conntrack.lookupTcp;
+    getFlags() == SYN -> lookupTcpListen), UdpInput.java:45-47 (ipPkt.getDst(), udpPkt.getDstPort()).
+    Fields as the parsers set them: Ipv4Packet.initPartial src/dst at 12 / 16 (Ipv4Packet.java:51-54),
+    Ipv6Packet at 8 / 24 (Ipv6Packet.java:47-50), Tcp/UdpPacket.initPartial ports at 0 / 2 and TCP
+    flags = uint16(12) & 0x3f (TcpPacket.java:192-195, UdpPacket.java:22-23).  Bytes in network order,
+    an IPv4 address in the first 4 of 16; a frame the parser refuses gives all zeros (l3_ver 0)."""
+    t = {"src": bytes(16), "dst": bytes(16), "sport": bytes(2), "dport": bytes(2), "l3_ver": 0, "l4_proto": 0,
+         "tcp_flags": 0}
+    info, err = parse_ether(frame)
+    if info is None:
+        return t
+    l3 = bytes(frame)[info.l3_off:info.l3_off + info.l3_len]
+    if info.ver == 4:
+        t["src"], t["dst"] = l3[12:16] + bytes(12), l3[16:20] + bytes(12)
+    else:
+        t["src"], t["dst"] = l3[8:24], l3[24:40]
+    t["l3_ver"], t["l4_proto"] = info.ver, info.proto
+    if info.proto in (IP_PROTOCOL_TCP, IP_PROTOCOL_UDP):
+        l4 = l3[info.l4_off:]
+        t["sport"], t["dport"] = l4[0:2], l4[2:4]
+        if info.proto == IP_PROTOCOL_TCP:
+            t["tcp_flags"] = _u16(l4, 12) & 0x3F
+    return t
+
+
 def pseudo_partial(l3: bytes, info: L3Info) -> int:
     """VPCSUM_F_L4P (checksum offload, XDPConsts.VP_CSUM_UP_PSEUDO): the folded, uncomplemented
     pseudo-header sum the L4 field holds for CHECKSUM_PARTIAL; Utils.calculateChecksumIntermediate

@@ -1121,3 +1121,51 @@ def test_nat_arena_beyond_4gib(V, orc):
     torch.cuda.empty_cache()
 
 
+
+
+def test_parse_tuples_match_oracle(V, orc):
+    """vpcsum_parse_ether_tuples_async (batched header parse + flow tuple)
+    against oracle.flow_tuple frame by frame: the reference's pcap and KAT frames, every edge frame
+    of the parse rules (tests/edgevec.py:parse_cases), and 4000 fuzzed IPv4/IPv6 TCP/UDP/ICMP
+    packets (options, IPv6 without extension headers) in Ethernet frames at odd offsets.  The
+    descriptors equal those of the plain parse."""
+    import torch
+    import edgevec as E
+    frames = [f for f, _, _ in E.parse_cases()]
+    for fn in sorted(os.listdir(os.path.join(GOLD, "pcap"))):
+        lt, pkts = read_pcap(os.path.join(GOLD, "pcap", fn))
+        if lt == 1:
+            frames += pkts
+    kats = json.load(open(os.path.join(GOLD, "kat.json")))["kats"]
+    frames += [bytes.fromhex(k["hex"]) for k in kats if k["layer"] == "ether"]
+    a, d = orc.synth(4000, 2048, 14, O.SYNTH_FUZZ, O.SEED, 4242)
+    for r in d:
+        l3 = bytes(a[int(r["l3_off"]):int(r["l3_off"]) + int(r["l3_len"])])
+        frames.append(bytes(12) + (b"\x08\x00" if r["l3_ver"] == 4 else b"\x86\xdd") + l3)
+    offs, lens, arena = [], [], bytearray()
+    for i, f in enumerate(frames):
+        arena += bytes(i % 5)
+        offs.append(len(arena))
+        lens.append(len(f))
+        arena += f
+    arena = np.frombuffer(bytes(arena) + bytes(64), np.uint8).copy()
+    n = len(frames)
+    ga, go, gl = dev(arena), dev(np.array(offs, np.uint64)), dev(np.array(lens, np.uint32))
+    d1 = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    d2 = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    tu = torch.full((n * V.TUPLE_DTYPE.itemsize,), 0xAB, dtype=torch.uint8, device="cuda")
+    V.parse_ether(ga, go, gl, n, d1)
+    V.parse_ether(ga, go, gl, n, d2, st, tuples=tu)
+    torch.cuda.synchronize()
+    assert torch.equal(d1, d2)
+    got = tu.cpu().numpy().view(V.TUPLE_DTYPE)
+    nacc = 0
+    for i, f in enumerate(frames):
+        w = O.flow_tuple(f)
+        g = got[i]
+        assert bytes(g["src"]) == w["src"] and bytes(g["dst"]) == w["dst"], i
+        assert bytes(g["sport"]) == w["sport"] and bytes(g["dport"]) == w["dport"], i
+        assert (g["l3_ver"], g["l4_proto"], g["tcp_flags"], g["rsv"]) == (w["l3_ver"], w["l4_proto"], w["tcp_flags"], 0), i
+        nacc += w["l3_ver"] != 0
+    assert nacc > 4000

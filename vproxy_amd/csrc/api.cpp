@@ -242,7 +242,20 @@ int vpcsum_parse_ether_async(const uint8_t* d_arena, uint64_t arena_len, const u
                              uint8_t* d_status, void* stream) {
     if (n == 0) return 0;
     if (!d_arena || !d_frame_off || !d_frame_len || !d_desc) return fail("vpcsum_parse_ether_async: NULL argument");
-    VPC_CHECK(launch_parse_ether(d_arena, arena_len, d_frame_off, d_frame_len, n, flags, d_desc, d_status,
+    VPC_CHECK(launch_parse_ether(d_arena, arena_len, d_frame_off, d_frame_len, n, flags, d_desc, d_status, nullptr,
+                                 (hipStream_t)stream),
+              "parse launch");
+    return 0;
+}
+
+int vpcsum_parse_ether_tuples_async(const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_frame_off,
+                                    const uint32_t* d_frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* d_desc,
+                                    uint8_t* d_status, vpcsum_tuple_t* d_tuples, void* stream) {
+    if (n == 0) return 0;
+    if (!d_arena || !d_frame_off || !d_frame_len || !d_desc || !d_tuples)
+        return fail("vpcsum_parse_ether_tuples_async: NULL argument");
+    if ((uintptr_t)d_tuples & 3) return fail("vpcsum_parse_ether_tuples_async: tuples not 4-byte aligned");
+    VPC_CHECK(launch_parse_ether(d_arena, arena_len, d_frame_off, d_frame_len, n, flags, d_desc, d_status, d_tuples,
                                  (hipStream_t)stream),
               "parse launch");
     return 0;
@@ -795,7 +808,7 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
         memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
         memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
         VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.d_desc,
-                                     nullptr, s.stream),
+                                     nullptr, nullptr, s.stream),
                   "parse launch");
         VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, s.dh_out, s.dh_status, nullptr, VPCSUM_MODE_VERIFY, nullptr,
                               n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),

@@ -1410,7 +1410,8 @@ __device__ bool pe_ipv6_from(const uint8_t* b, uint32_t avail, uint32_t& total, 
 __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                     const uint64_t* __restrict__ foff,
                                                     const uint32_t* __restrict__ flen, uint32_t n, uint8_t want,
-                                                    vpcsum_desc_t* __restrict__ desc, uint8_t* __restrict__ status) {
+                                                    vpcsum_desc_t* __restrict__ desc, uint8_t* __restrict__ status,
+                                                    vpcsum_tuple_t* __restrict__ tuples) {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const uint64_t o = foff[p];
         const uint32_t L = flen[p];
@@ -1471,17 +1472,45 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
         }
         desc[p] = d;
         if (status) status[p] = st;
+        if (tuples) {
+            // the flow tuple the L4 input nodes read (vpcsum.h vpcsum_tuple_t): addresses at
+            // Ipv4Packet :51-54 (12, 16) / Ipv6Packet :47-50 (8, 24), ports and TCP flags at
+            // TcpPacket / UdpPacket.initPartial (0, 2, 12); zeros for a refused frame
+            uint32_t t[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+            if (st == 0) {
+                const uint8_t* b = arena + d.l3_off;
+                auto put = [&](int dw0, const uint8_t* src, int nb) {   // bytes in memory order
+                    for (int k = 0; k < nb; ++k) t[dw0 + (k >> 2)] |= (uint32_t)src[k] << (8 * (k & 3));
+                };
+                if (d.l3_ver == 4) {
+                    put(0, b + 12, 4);
+                    put(4, b + 16, 4);
+                } else {
+                    put(0, b + 8, 16);
+                    put(4, b + 24, 16);
+                }
+                const uint8_t* l4 = b + d.l4_off;
+                uint32_t w8 = d.l3_ver | ((uint32_t)d.l4_proto << 8);
+                if (d.l4_proto == 6 || d.l4_proto == 17) {   // accepted: at least 8 / 20 bytes
+                    put(8, l4, 4);
+                    if (d.l4_proto == 6) w8 |= (uint32_t)(l4[13] & 0x3f) << 16;
+                }
+                t[9] = w8;
+            }
+            uint32_t* qw = (uint32_t*)(tuples + p);   // 40 B, 4-B aligned (checked by the API)
+            for (int k = 0; k < 10; ++k) qw[k] = t[k];
+        }
     }
 }
 
 hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const uint64_t* frame_off,
                               const uint32_t* frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* desc,
-                              uint8_t* status, hipStream_t stream) {
+                              uint8_t* status, vpcsum_tuple_t* tuples, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     uint32_t g = (n + 255) / 256;
     if (g > 65535u * 8) g = 65535u * 8;
     hipLaunchKernelGGL(k_parse_ether, dim3(g), dim3(256), 0, stream, arena, arena_len, frame_off, frame_len, n,
-                       flags, desc, status);
+                       flags, desc, status, tuples);
     return hipGetLastError();
 }
 

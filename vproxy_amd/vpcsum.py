@@ -29,11 +29,15 @@ NAT4_DTYPE = np.dtype([("src", "u1", 4), ("dst", "u1", 4), ("sport", "u1", 2), (
                        ("mask", "u1"), ("rsv", "u1", 3)])
 NAT_DTYPE = np.dtype([("src", "u1", 16), ("dst", "u1", 16), ("sport", "u1", 2), ("dport", "u1", 2),
                       ("mask", "u1"), ("ttl", "u1"), ("rsv", "u1", 10)])
+# vpcsum_tuple_t: the flow tuple of a parsed frame (network-order addresses and ports)
+TUPLE_DTYPE = np.dtype([("src", "u1", 16), ("dst", "u1", 16), ("sport", "u1", 2), ("dport", "u1", 2),
+                        ("l3_ver", "u1"), ("l4_proto", "u1"), ("tcp_flags", "u1"), ("rsv", "u1")])
 
 # Every symbol include/vpcsum.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "vpcsum_abi_version", "vpcsum_last_error", "vpcsum_device_count", "vpcsum_set_device",
-    "vpcsum_compute_async", "vpcsum_nat4_async", "vpcsum_nat_async", "vpcsum_parse_ether_async", "vpcsum_read_probe_async",
+    "vpcsum_compute_async", "vpcsum_nat4_async", "vpcsum_nat_async", "vpcsum_parse_ether_async",
+    "vpcsum_parse_ether_tuples_async", "vpcsum_read_probe_async",
     "vpcsum_pattern_probe_async",
     "vpcsum_synth_async", "vpcsum_event_create", "vpcsum_event_destroy", "vpcsum_event_record",
     "vpcsum_event_elapsed_ms", "vpcsum_stream_sync", "vpcsum_ctx_create", "vpcsum_ctx_destroy",
@@ -79,6 +83,7 @@ def _declare(L):
         "vpcsum_group_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
         "vpcsum_group_wait": ([P, U64], I),
         "vpcsum_parse_ether_async": ([P, U64, P, P, U32, U8, P, P, P], I),
+        "vpcsum_parse_ether_tuples_async": ([P, U64, P, P, U32, U8, P, P, P, P], I),
         "vpcsum_read_probe_async": ([P, U64, P, U32, P], I),
         "vpcsum_pattern_probe_async": ([P, U64, P, U32, P, U32, P], I),
         "vpcsum_synth_async": ([P, U64, U32, U32, U32, U32, U64, U64, P, P], I),
@@ -176,9 +181,18 @@ def nat(arena, desc, rw, n: int, status=None, nat_mode: int = NAT_RFC1624, strea
                                   _stream(stream)), "vpcsum_nat_async")
 
 
-def parse_ether(arena, frame_off, frame_len, n: int, desc, status=None, flags: int = F_IP | F_L4, stream=None):
-    _check(lib().vpcsum_parse_ether_async(_ptr(arena), arena.numel(), _ptr(frame_off), _ptr(frame_len), n, flags,
-                                          _ptr(desc), _ptr(status), _stream(stream)), "vpcsum_parse_ether_async")
+def parse_ether(arena, frame_off, frame_len, n: int, desc, status=None, flags: int = F_IP | F_L4, stream=None,
+                tuples=None):
+    """Descriptors from raw frames on the GPU; with `tuples` (n x 40 bytes, TUPLE_DTYPE) also each
+    frame's flow tuple (vpcsum_parse_ether_tuples_async)."""
+    if tuples is None:
+        _check(lib().vpcsum_parse_ether_async(_ptr(arena), arena.numel(), _ptr(frame_off), _ptr(frame_len), n, flags,
+                                              _ptr(desc), _ptr(status), _stream(stream)), "vpcsum_parse_ether_async")
+        return
+    assert tuples.numel() * tuples.element_size() >= n * TUPLE_DTYPE.itemsize
+    _check(lib().vpcsum_parse_ether_tuples_async(_ptr(arena), arena.numel(), _ptr(frame_off), _ptr(frame_len), n,
+                                                 flags, _ptr(desc), _ptr(status), _ptr(tuples), _stream(stream)),
+           "vpcsum_parse_ether_tuples_async")
 
 
 def pattern_probe(arena, desc, n: int, sink, grid: int = 0, stream=None):
