@@ -10,7 +10,9 @@ Two restatements of vproxy's Java checksum code, used only by ``tests/``,
   batches and for the timed CPU baseline.
 * :func:`parse_ether` / :func:`parse_l3` ... restatement of the parse rules that decide the
   checksum inputs (EthernetPacket.from, EthernetPacket.java:25-94; Ipv4Packet.from,
-  Ipv4Packet.java:73-145; Ipv6Packet.from, Ipv6Packet.java:69-159) producing descriptors.
+  Ipv4Packet.java:73-145; Ipv6Packet.from, Ipv6Packet.java:69-159) producing descriptors, and
+  :func:`flow_tuple`, the conntrack key the L4 input nodes read (TcpInput.java:47-51,
+  UdpInput.java:45-47).
 
 Parity pin: tests/test_oracle_golden.py checks this module against every TestPacket.java
 known-answer vector and the reference's pcap fixtures (tests/golden/).
