@@ -1412,13 +1412,20 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
                                                     const uint32_t* __restrict__ flen, uint32_t n, uint8_t want,
                                                     vpcsum_desc_t* __restrict__ desc, uint8_t* __restrict__ status,
                                                     vpcsum_tuple_t* __restrict__ tuples) {
-    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
-        const uint64_t o = foff[p];
-        const uint32_t L = flen[p];
+    // 64 tuples of a wave are staged here and written as 10 coalesced 256-B stores
+    __shared__ uint32_t s_tu[256 * 10];
+    const uint32_t ln = threadIdx.x & 63u;
+    // q: the wave's first frame (wave-uniform, so that every lane of the wave reaches the
+    // tuple exchange, also in the batch's last, partial wave)
+    for (uint32_t q = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); q < n; q += gridDim.x * blockDim.x) {
+        const uint32_t p = q + ln;
+        const bool act = p < n;
+        const uint64_t o = act ? foff[p] : 0;
+        const uint32_t L = act ? flen[p] : 0;
         vpcsum_desc_t d;
         d.l3_off = 0; d.l3_len = 0; d.l4_off = 0; d.l3_ver = 0; d.l4_proto = 0; d.flags = 0; d.rsv = 0;
         uint8_t st = VPCSUM_S_BAD_DESC;
-        bool ok = o <= arena_len && (uint64_t)L <= arena_len - o && L >= 14;
+        bool ok = act && o <= arena_len && (uint64_t)L <= arena_len - o && L >= 14;
         const uint8_t* f = arena + o;
         uint32_t hl = 14, typ = 0;
         if (ok) {
@@ -1470,8 +1477,10 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
                 fl |= VPCSUM_F_L4;
             d.flags = fl;
         }
-        desc[p] = d;
-        if (status) status[p] = st;
+        if (act) {
+            desc[p] = d;
+            if (status) status[p] = st;
+        }
         if (tuples) {
             // the flow tuple the L4 input nodes read (vpcsum.h vpcsum_tuple_t): addresses at
             // Ipv4Packet :51-54 (12, 16) / Ipv6Packet :47-50 (8, 24), ports and TCP flags at
@@ -1497,8 +1506,16 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
                 }
                 t[9] = w8;
             }
-            uint32_t* qw = (uint32_t*)(tuples + p);   // 40 B, 4-B aligned (checked by the API)
-            for (int k = 0; k < 10; ++k) qw[k] = t[k];
+            uint32_t* wt = s_tu + (threadIdx.x & ~63u) * 10;   // this wave's 64 x 10 dwords
+            for (int k = 0; k < 10; ++k) wt[ln * 10 + k] = t[k];
+            wave_sync_lds();
+            uint32_t* dst = (uint32_t*)(tuples + q);   // 4-B aligned (checked by the API)
+            const uint32_t nd = min(64u, n - q) * 10u;
+            for (uint32_t j = 0; j < 10; ++j) {
+                const uint32_t i = j * 64u + ln;
+                if (i < nd) dst[i] = wt[i];
+            }
+            wave_sync_lds();   // the slots are rewritten by the wave's next frames
         }
     }
 }
