@@ -253,6 +253,16 @@ int vpcsum_ctx_stats(vpcsum_ctx_t* ctx, uint64_t* service_batches, uint64_t* ser
 int vpcsum_ctx_verify_frames(vpcsum_ctx_t* ctx, const uint8_t* h_arena, uint64_t arena_len,
                              const uint64_t* h_frame_off, const uint32_t* h_frame_len, uint32_t n,
                              uint32_t* h_out, uint8_t* h_status, uint64_t* ticket);
+/* Batched parse of a received batch with flow tuples (the conntrack key TcpInput / UdpInput read,
+ * TcpInput.java:47-51, UdpInput.java:45-47): the frames of a registered arena, as for
+ * vpcsum_ctx_verify_frames, are parsed on the GPU where they lie; at vpcsum_ctx_wait h_desc[i]
+ * holds frame i's descriptor (l3_off relative to h_arena, flags F_IP | F_L4 as the frame allows),
+ * h_status[i] 0 or S_BAD_DESC, h_tuples[i] its vpcsum_tuple_t (any of the three may be NULL).
+ * The descriptors can go straight to vpcsum_ctx_submit / vpcsum_ctx_nat_submit. */
+int vpcsum_ctx_parse_frames(vpcsum_ctx_t* ctx, const uint8_t* h_arena, uint64_t arena_len,
+                            const uint64_t* h_frame_off, const uint32_t* h_frame_len, uint32_t n,
+                            vpcsum_desc_t* h_desc, uint8_t* h_status, vpcsum_tuple_t* h_tuples,
+                            uint64_t* ticket);
 /* NAT / TTL rewrites of host frames (SwitchUtils.applyNat for a batch): h_rw[i] rewrites the
  * packet of h_desc[i] in place in the caller's frames, with the checksums updated as Java's
  * recompute leaves them (nat_mode as vpcsum_nat_async).  Frames in a registered arena are
@@ -326,6 +336,12 @@ int Java_io_vproxy_vpcsum_VPCsum_submit(PNIEnv_vpcsum_long* env, int64_t ctx, vo
  *                     MemorySegment frameLen, int n, MemorySegment out, MemorySegment status) -> long ticket */
 int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                               void* frameOff, void* frameLen, int32_t n, void* out, void* status);
+/* VPCsum.parseFrames(long ctx, MemorySegment arena, long arenaLen, MemorySegment frameOff,
+ *                    MemorySegment frameLen, int n, MemorySegment desc, MemorySegment status,
+ *                    MemorySegment tuples) -> long ticket */
+int Java_io_vproxy_vpcsum_VPCsum_parseFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                             void* frameOff, void* frameLen, int32_t n, void* desc, void* status,
+                                             void* tuples);
 /* VPCsum.natSubmit(long ctx, MemorySegment arena, long arenaLen, MemorySegment desc,
  *                  MemorySegment rw, int n, MemorySegment status, int natMode) -> long ticket */
 int Java_io_vproxy_vpcsum_VPCsum_natSubmit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,

@@ -189,6 +189,19 @@ public final class GpuCsumBatch implements AutoCloseable {
         return status;
     }
 
+    /**
+     * Parse of a received batch with flow tuples (XDPIface.readable, then TcpInput / UdpInput's
+     * conntrack lookups, TcpInput.java:47-51, UdpInput.java:45-47): {@code count} frames at umem
+     * offsets {@code frameOff} (u64) with lengths {@code frameLen} (u32).  Fills {@code desc}
+     * (16 B per frame, usable by {@link #nat} and {@link #verify}), {@code parseStatus} (0 or
+     * S_BAD_DESC) and {@code tuples} (40 B per frame).
+     */
+    public void parseFrames(MemorySegment frameOff, MemorySegment frameLen, int count, MemorySegment desc,
+                            MemorySegment parseStatus, MemorySegment tuples) throws IOException {
+        long t = VPCsum.get().parseFrames(env, ctx, umem, umemLen, frameOff, frameLen, count, desc, parseStatus, tuples);
+        VPCsum.get().waitFor(env, ctx, t);
+    }
+
     @Override
     public void close() {
         VPCsum.get().close(env, ctx);

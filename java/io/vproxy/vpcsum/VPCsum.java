@@ -16,7 +16,7 @@ import java.lang.invoke.MethodHandle;
  *
  * No method is linked critical ({@code setCritical(false)} throughout): every entry point may
  * block -- create / registerArena allocate and page-lock through the HIP runtime, submit /
- * natSubmit / verifyFrames finish the batch that last used their slot (an event wait, or the
+ * natSubmit / verifyFrames / parseFrames finish the batch that last used their slot (an event wait, or the
  * service grid's completion), waitFor and setService wait by design.  A critical downcall keeps
  * the thread in Java state and would stall every safepoint (GC included) for that long.
  *
@@ -160,6 +160,34 @@ public class VPCsum {
         int ERR;
         try {
             ERR = (int) verifyFramesMH.invokeExact(ENV.MEMORY, ctx, arena, arenaLen, frameOff, frameLen, n, out, status);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+        return ENV.returnLong();
+    }
+
+    private static final MethodHandle parseFramesMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
+        "Java_io_vproxy_vpcsum_VPCsum_parseFrames", long.class /* ctx */, MemorySegment.class /* arena */,
+        long.class /* arenaLen */, MemorySegment.class /* frameOff */, MemorySegment.class /* frameLen */, int.class /* n */,
+        MemorySegment.class /* desc */, MemorySegment.class /* status */, MemorySegment.class /* tuples */);
+
+    /** Batched parse of a received batch with flow tuples: the frames at frameOff[i] / frameLen[i]
+     * of the registered {@code arena} are parsed on the GPU (EthernetPacket/Ipv4Packet/Ipv6Packet
+     * rules).  After {@link #waitFor}: desc[i] (16 B, ready for submit / natSubmit), status[i]
+     * (0 or S_BAD_DESC) and tuples[i] (40 B: src[16] dst[16] sport[2] dport[2] ver proto
+     * tcpFlags rsv, network order), the key TcpInput / UdpInput look up in the conntrack
+     * (TcpInput.java:47-51, UdpInput.java:45-47).  Returns a ticket. */
+    public long parseFrames(PNIEnv ENV, long ctx, MemorySegment arena, long arenaLen, MemorySegment frameOff,
+                            MemorySegment frameLen, int n, MemorySegment desc, MemorySegment status,
+                            MemorySegment tuples) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) parseFramesMH.invokeExact(ENV.MEMORY, ctx, arena, arenaLen, frameOff, frameLen, n, desc, status, tuples);
         } catch (Throwable THROWABLE) {
             throw PanamaUtils.convertInvokeExactException(THROWABLE);
         }

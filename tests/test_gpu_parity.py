@@ -1169,3 +1169,48 @@ def test_parse_tuples_match_oracle(V, orc):
         assert (g["l3_ver"], g["l4_proto"], g["tcp_flags"], g["rsv"]) == (w["l3_ver"], w["l4_proto"], w["tcp_flags"], 0), i
         nacc += w["l3_ver"] != 0
     assert nacc > 4000
+
+
+def test_ctx_parse_frames_tuples(V, orc):
+    """vpcsum_ctx_parse_frames (PNI parseFrames, GpuCsumBatch.parseFrames): an RX batch in a
+    registered arena parsed where it lies, with flow tuples; descriptors, status and tuples equal
+    the oracle's, and the descriptors verify the frames through vpcsum_ctx_submit as the
+    reference's recompute does.  Two batches back to back exercise both slots."""
+    import edgevec as E
+    frames = [f for f, _, _ in E.parse_cases()]
+    a, d = orc.synth(600, 2048, 14, O.SYNTH_FUZZ, O.SEED, 99)
+    for r in d:
+        l3 = bytes(a[int(r["l3_off"]):int(r["l3_off"]) + int(r["l3_len"])])
+        frames.append(bytes(12) + (b"\x08\x00" if r["l3_ver"] == 4 else b"\x86\xdd") + l3)
+    offs, lens, arena = [], [], bytearray()
+    for i, f in enumerate(frames):
+        arena += bytes(3 if i % 2 else 0)
+        offs.append(len(arena))
+        lens.append(len(f))
+        arena += f
+    arena = np.frombuffer(bytes(arena) + bytes(64), np.uint8).copy()
+    n = len(frames)
+    ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=n)
+    ctx.register(arena)
+    for rep in range(2):
+        desc, st, tu = ctx.parse_frames(arena, np.array(offs), np.array(lens))
+        for i, f in enumerate(frames):
+            info, _ = O.parse_ether(f)
+            w = O.flow_tuple(f)
+            if info is None:
+                assert st[i] == O.S_BAD_DESC and tu[i]["l3_ver"] == 0, i
+                continue
+            assert st[i] == 0
+            g = desc[i]
+            assert int(g["l3_off"]) == offs[i] + info.l3_off
+            assert (g["l3_len"], g["l4_off"], g["l3_ver"], g["l4_proto"], g["flags"]) == \
+                (info.l3_len, info.l4_off, info.ver, info.proto, O.desc_flags_for(info))
+            assert bytes(tu[i]["src"]) == w["src"] and bytes(tu[i]["dst"]) == w["dst"], i
+            assert bytes(tu[i]["sport"]) == w["sport"] and bytes(tu[i]["dport"]) == w["dport"], i
+            assert (tu[i]["l4_proto"], tu[i]["tcp_flags"]) == (w["l4_proto"], w["tcp_flags"]), i
+    ok = st == 0
+    good = np.ascontiguousarray(desc[ok])
+    vout, vst = ctx.run(arena, good, O.MODE_VERIFY)
+    want, want_st = orc.process(arena, good, O.MODE_VERIFY)
+    ctx.close()
+    assert np.array_equal(vout, want) and np.array_equal(vst, want_st)

@@ -81,9 +81,11 @@ struct Slot {
     vpcsum_nat_t* h_rw = nullptr;      // NAT rewrite tables: pinned staging (mapped) and device copy,
     vpcsum_nat_t* dh_rw = nullptr;     // allocated with the context's first NAT batch
     vpcsum_nat_t* d_rw = nullptr;
+    vpcsum_tuple_t* h_tu = nullptr;    // flow tuples of a parse batch: pinned (mapped), allocated
+    vpcsum_tuple_t* dh_tu = nullptr;   // with the context's first parse batch
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
-    int kind = 0;                      // current batch: 0 checksums, 1 NAT rewrite
+    int kind = 0;                      // current batch: 0 checksums, 1 NAT rewrite, 2 parse
     bool zero_copy = false;            // current batch ran on the host frames in place
     uint32_t svc_seq = 0;              // != 0: the batch went to the low-latency service
     // the batch currently owned by this slot
@@ -95,6 +97,8 @@ struct Slot {
     const vpcsum_desc_t* user_desc = nullptr;
     uint32_t* user_out = nullptr;
     uint8_t* user_status = nullptr;
+    vpcsum_desc_t* user_desc_out = nullptr;   // parse batch: where descriptors and tuples go
+    vpcsum_tuple_t* user_tuples = nullptr;
 };
 
 }  // namespace vpcsum
@@ -334,6 +338,7 @@ static void slot_free(Slot& s) {
     if (s.h_flen) (void)hipHostFree(s.h_flen);
     if (s.h_rw) (void)hipHostFree(s.h_rw);
     if (s.d_rw) (void)hipFree(s.d_rw);
+    if (s.h_tu) (void)hipHostFree(s.h_tu);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot();
@@ -594,6 +599,13 @@ static int slot_finish(vpcsum_ctx* c, Slot& s) {
         s.busy = false;
         return 0;
     }
+    if (s.kind == 2) {   // parse: descriptors, status and tuples were written to the pinned staging
+        if (s.user_desc_out) memcpy(s.user_desc_out, s.h_desc, (size_t)s.n * sizeof(vpcsum_desc_t));
+        if (s.user_status) memcpy(s.user_status, s.h_status, s.n);
+        if (s.user_tuples) memcpy(s.user_tuples, s.h_tu, (size_t)s.n * sizeof(vpcsum_tuple_t));
+        s.busy = false;
+        return 0;
+    }
     const uint32_t* res_out = s.svc_seq ? c->svc.h_out : s.h_out;
     const uint8_t* res_status = s.svc_seq ? c->svc.h_status : s.h_status;
     if (s.user_out) memcpy(s.user_out, res_out, (size_t)s.n * 4);
@@ -826,6 +838,55 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
     s.user_desc = nullptr;
     s.user_out = h_out;
     s.user_status = h_status;
+    *ticket = t;
+    return 0;
+}
+
+int vpcsum_ctx_parse_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
+                            const uint32_t* h_frame_len, uint32_t n, vpcsum_desc_t* h_desc, uint8_t* h_status,
+                            vpcsum_tuple_t* h_tuples, uint64_t* ticket) {
+    if (!c || !ticket) return fail("vpcsum_ctx_parse_frames: NULL context or ticket");
+    if (n > c->max_pkts) return fail("vpcsum_ctx_parse_frames: %u frames > capacity %u", n, c->max_pkts);
+    if (n && (!h_arena || !h_frame_off || !h_frame_len)) return fail("vpcsum_ctx_parse_frames: NULL arena or frame table");
+    std::lock_guard<std::mutex> lk(c->mu);
+    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
+    if (n && !base) return fail("vpcsum_ctx_parse_frames: the arena must be registered (vpcsum_ctx_register_arena)");
+    const uint64_t t = c->next_ticket++;
+    Slot& s = c->slots[t & 1];
+    if (s.busy && slot_finish(c, s) != 0) return -1;
+    if (!s.h_tu) {
+        hipError_t e = hipHostMalloc((void**)&s.h_tu, (size_t)c->max_pkts * sizeof(vpcsum_tuple_t),
+                                     hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s.dh_tu, s.h_tu, 0);
+        if (e != hipSuccess) {
+            if (s.h_tu) (void)hipHostFree(s.h_tu);
+            s.h_tu = s.dh_tu = nullptr;
+            return hipfail(e, "vpcsum_ctx_parse_frames allocation");
+        }
+    }
+    if (n) {
+        // parsed where the frames lie (zero-copy); results straight into the pinned staging
+        memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
+        memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
+        VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.dh_desc,
+                                     s.dh_status, s.dh_tu, s.stream),
+                  "parse launch");
+    }
+    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+    s.zero_copy = true;
+    s.svc_seq = 0;
+    s.kind = 2;
+    s.busy = true;
+    s.ticket = t;
+    s.n = n;
+    s.mode = 0;
+    s.user_arena = nullptr;
+    s.user_desc = nullptr;
+    s.user_out = nullptr;
+    s.user_status = h_status;
+    s.user_desc_out = h_desc;
+    s.user_tuples = h_tuples;
     *ticket = t;
     return 0;
 }
@@ -1180,6 +1241,22 @@ int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t c
     if (vpcsum_ctx_verify_frames((vpcsum_ctx_t*)(intptr_t)ctx, (const uint8_t*)arena, (uint64_t)arenaLen,
                                  (const uint64_t*)frameOff, (const uint32_t*)frameLen, (uint32_t)n, (uint32_t*)out,
                                  (uint8_t*)status, &t) != 0)
+        return pni_throw(env, "java.io.IOException");
+    env->return_ = (int64_t)t;
+    return 0;
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_parseFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                             void* frameOff, void* frameLen, int32_t n, void* desc, void* status,
+                                             void* tuples) {
+    if (n < 0 || arenaLen < 0) {
+        fail("parseFrames: negative size");
+        return pni_throw(env, "java.lang.IllegalArgumentException");
+    }
+    uint64_t t = 0;
+    if (vpcsum_ctx_parse_frames((vpcsum_ctx_t*)(intptr_t)ctx, (const uint8_t*)arena, (uint64_t)arenaLen,
+                                (const uint64_t*)frameOff, (const uint32_t*)frameLen, (uint32_t)n,
+                                (vpcsum_desc_t*)desc, (uint8_t*)status, (vpcsum_tuple_t*)tuples, &t) != 0)
         return pni_throw(env, "java.io.IOException");
     env->return_ = (int64_t)t;
     return 0;

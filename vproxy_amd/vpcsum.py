@@ -43,13 +43,14 @@ EXPORTS = [
     "vpcsum_event_elapsed_ms", "vpcsum_stream_sync", "vpcsum_ctx_create", "vpcsum_ctx_destroy",
     "vpcsum_ctx_register_arena", "vpcsum_ctx_unregister_arena", "vpcsum_ctx_submit", "vpcsum_ctx_wait",
     "vpcsum_ctx_pipeline", "vpcsum_ctx_set_service", "vpcsum_ctx_stats", "vpcsum_ctx_verify_frames",
+    "vpcsum_ctx_parse_frames",
     "vpcsum_ctx_nat_submit", "Java_io_vproxy_vpcsum_VPCsum_natSubmit",
     "vpcsum_group_create", "vpcsum_group_create_list", "vpcsum_group_destroy", "vpcsum_group_register_arena",
     "vpcsum_group_submit", "vpcsum_group_wait",
     "Java_io_vproxy_vpcsum_VPCsum_create", "Java_io_vproxy_vpcsum_VPCsum_registerArena",
     "Java_io_vproxy_vpcsum_VPCsum_submit", "Java_io_vproxy_vpcsum_VPCsum_waitFor",
     "Java_io_vproxy_vpcsum_VPCsum_close", "Java_io_vproxy_vpcsum_VPCsum_setService",
-    "Java_io_vproxy_vpcsum_VPCsum_verifyFrames",
+    "Java_io_vproxy_vpcsum_VPCsum_verifyFrames", "Java_io_vproxy_vpcsum_VPCsum_parseFrames",
 ]
 
 
@@ -99,6 +100,7 @@ def _declare(L):
         "vpcsum_ctx_set_service": ([P, U32], I),
         "vpcsum_ctx_stats": ([P, P, P], I),
         "vpcsum_ctx_verify_frames": ([P, P, U64, P, P, U32, P, P, P], I),
+        "vpcsum_ctx_parse_frames": ([P, P, U64, P, P, U32, P, P, P, P], I),
         "vpcsum_ctx_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
         "vpcsum_ctx_wait": ([P, U64], I),
         "vpcsum_ctx_pipeline": ([P, P, U32, U32, P, U32, P, U32, U32], I),
@@ -284,6 +286,22 @@ class Context:
                "vpcsum_ctx_verify_frames")
         self.wait(t.value)
         return out, status
+
+    def parse_frames(self, arena: np.ndarray, frame_off: np.ndarray, frame_len: np.ndarray):
+        """Batched parse of received Ethernet frames in a registered arena, with flow tuples
+        (vpcsum_ctx_parse_frames).  Returns (descriptors, status, tuples) per frame."""
+        n = len(frame_off)
+        fo = np.ascontiguousarray(frame_off, dtype=np.uint64)
+        fl = np.ascontiguousarray(frame_len, dtype=np.uint32)
+        desc = np.zeros(n, DESC_DTYPE)
+        status = np.zeros(n, np.uint8)
+        tuples = np.zeros(n, TUPLE_DTYPE)
+        t = ctypes.c_uint64()
+        _check(lib().vpcsum_ctx_parse_frames(self.h, arena.ctypes.data, arena.nbytes, fo.ctypes.data, fl.ctypes.data,
+                                             n, desc.ctypes.data, status.ctypes.data, tuples.ctypes.data,
+                                             ctypes.byref(t)), "vpcsum_ctx_parse_frames")
+        self.wait(t.value)
+        return desc, status, tuples
 
     def nat_submit(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray, status: np.ndarray | None = None,
                    nat_mode: int = NAT_RFC1624) -> int:
