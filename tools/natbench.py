@@ -33,6 +33,42 @@ for name, mode in modes:
     ms = e0.elapsed_ms(e1) / it
     res[name] = {"ms": round(ms, 4), "Mpps": round(n / ms / 1e3, 1), "GBps_at_72B": round(n * 72 / ms / 1e6, 1)}
 
+if "--v6" in sys.argv:
+    # 48-B entries (vpcsum_nat_async): the same IPv4 batch, and 1M IPv6/TCP packets of 9000 B (C4
+    # frames) with 16-B addresses and ports rewritten, RFC 1624
+    def timed48(ar, dd, rw48, m, mode):
+        s_ = torch.zeros(m, dtype=torch.uint8, device="cuda")
+        for _ in range(3):
+            V.nat(ar, dd, rw48, m, s_, mode)
+        e0, e1 = V.Event(), V.Event()
+        e0.record()
+        for _ in range(10):
+            V.nat(ar, dd, rw48, m, s_, mode)
+        e1.record()
+        torch.cuda.synchronize()
+        ms_ = e0.elapsed_ms(e1) / 10
+        assert int((s_ & V.S_BAD_DESC).sum().item()) == 0
+        return {"ms": round(ms_, 4), "Mpps": round(m / ms_ / 1e3, 1)}
+
+    def entries48(m, seed):
+        g_ = torch.Generator(device="cpu").manual_seed(seed)
+        r48 = torch.zeros((m, 48), dtype=torch.uint8)
+        r48[:, :36] = torch.randint(0, 256, (m, 36), dtype=torch.uint8, generator=g_)
+        r48[:, 36] = V.NAT_SRC | V.NAT_DST | V.NAT_SPORT | V.NAT_DPORT
+        return r48.cuda()
+
+    res["v4_48B_entries_rfc1624"] = timed48(arena, d, entries48(n, 6), n, V.NAT_RFC1624)
+    del arena
+    torch.cuda.empty_cache()
+    n6, s6 = 1 << 20, 9216
+    a6 = torch.zeros(n6 * s6, dtype=torch.uint8, device="cuda")
+    d6 = torch.zeros(n6 * 16, dtype=torch.uint8, device="cuda")
+    V.synth(a6, n6, s6, 0, V.SYNTH_C4, 0x20241020, 0, d6)
+    V.compute(a6, d6, n6, None, None, V.MODE_WRITE)
+    res["v6_c4_frames"] = {"packets": n6, "rfc1624": timed48(a6, d6, entries48(n6, 7), n6, V.NAT_RFC1624)}
+    print(json.dumps(res))
+    sys.exit(0)
+
 if "--no-cpu" not in sys.argv:
     # CPU baseline (BASELINE C5): the oracle's Java-semantics rewrite (setters + full recompute,
     # SwitchUtils.java:522-542) on a bounded sample of the same workload, 1 and 16 threads
