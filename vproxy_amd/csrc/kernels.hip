@@ -1489,7 +1489,12 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
             if (st == 0) {
                 const uint8_t* b = arena + d.l3_off;
                 auto put = [&](int dw0, const uint8_t* src, int nb) {   // bytes in memory order
-                    for (int k = 0; k < nb; ++k) t[dw0 + (k >> 2)] |= (uint32_t)src[k] << (8 * (k & 3));
+                    if (!((uintptr_t)src & 1)) {   // halfword loads where the field is 2-B aligned
+                        const uint16_t* h = (const uint16_t*)src;
+                        for (int k = 0; k < nb / 2; ++k) t[dw0 + (k >> 1)] |= (uint32_t)h[k] << (16 * (k & 1));
+                    } else {
+                        for (int k = 0; k < nb; ++k) t[dw0 + (k >> 2)] |= (uint32_t)src[k] << (8 * (k & 3));
+                    }
                 };
                 if (d.l3_ver == 4) {
                     put(0, b + 12, 4);
