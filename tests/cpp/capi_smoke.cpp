@@ -110,6 +110,25 @@ int main() {
             CHECK(st[0] == (VPCSUM_S_DONE | VPCSUM_S_IP_OK | VPCSUM_S_L4_OK) && st[1] == st[0], "after nat %02x %02x", st[0], st[1]);
         }
     }
+    // RX parse with flow tuples through the PNI entry (TcpInput / UdpInput's conntrack key) on the
+    // NAT'ed frames of the registered arena: dst 1.2.3.4 and source port 121 on both, SYN on the TCP one
+    uint64_t foff[2] = {0, 2048};
+    uint32_t flen[2] = {(uint32_t)udp.size(), (uint32_t)syn.size()};
+    vpcsum_desc_t pd[2];
+    vpcsum_tuple_t tu[2];
+    memset(&envl, 0, sizeof(envl));
+    CHECK(Java_io_vproxy_vpcsum_VPCsum_parseFrames(&envl, h, arena.data(), (int64_t)arena.size(), foff, flen, 2, pd, st, tu) == 0,
+          "pni parseFrames");
+    CHECK(Java_io_vproxy_vpcsum_VPCsum_waitFor(&envv, h, envl.return_) == 0, "parse wait");
+    CHECK(st[0] == 0 && st[1] == 0, "parse status %02x %02x", st[0], st[1]);
+    CHECK(pd[0].l3_off == 14 && pd[0].l3_len == 0x59 && pd[0].l4_proto == 17 && pd[1].l3_off == 2048 + 14 && pd[1].l4_proto == 6,
+          "parsed descriptors");
+    for (int i = 0; i < 2; ++i) {
+        CHECK(tu[i].l3_ver == 4 && tu[i].dst[0] == 1 && tu[i].dst[3] == 4 && tu[i].sport[0] == 0 && tu[i].sport[1] == 121,
+              "tuple %d", i);
+    }
+    CHECK(tu[0].src[0] == 0xc0 && tu[0].dport[0] == 0xc9 && tu[0].dport[1] == 0x14 && tu[0].tcp_flags == 0, "udp tuple");
+    CHECK(tu[1].src[0] == 0x0a && tu[1].dport[0] == 0x01 && tu[1].dport[1] == 0xbb && tu[1].tcp_flags == 0x02, "syn tuple");
     memset(&envl, 0, sizeof(envl));
     CHECK(Java_io_vproxy_vpcsum_VPCsum_create(&envl, 0, -1, 64) == -1, "pni bad args");
     CHECK(envl.ex.type && strcmp(envl.ex.type, "java.lang.IllegalArgumentException") == 0, "ex type");
