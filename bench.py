@@ -169,17 +169,18 @@ def oracle_sample_gate(synth_id: int, stride: int, first: int, out_np: np.ndarra
             "sample_equal": bool(np.array_equal(out_np[off:off + m], want))}
 
 
-def pmc_traffic(tag: str):
+def pmc_traffic(tag: str, packets: int):
     """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC summary
-    (profiles/r*_pmc_<tag>/summary.json, tools/traffic.py: FETCH_SIZE x 2 + WRITE_SIZE per
-    MI355X_MICROARCH.md §HBM).  PMC counters cannot be read from inside this process, so the
-    value comes from that separate --pmc run of the same kernel and config."""
+    (profiles/r*_pmc_<tag>/summary.json, tools/save_profiles.py: 2 x FETCH_SIZE + WRITE_SIZE, every
+    read request being 128 B), scaled from the summary's packet count to this rank's `packets` (a
+    strong shard holds part of the batch).  PMC counters cannot be read from inside this process,
+    so the value comes from that separate --pmc run of the same kernel and config."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{tag}", "summary.json")))
     for f in reversed(files):
         d = json.load(open(f))
-        if "hbm_bytes_per_launch" in d:
-            return int(d["hbm_bytes_per_launch"]), os.path.relpath(f, REPO)
+        if "hbm_bytes_per_launch" in d and d.get("packets"):
+            return int(round(d["hbm_bytes_per_launch"] * packets / d["packets"])), os.path.relpath(f, REPO)
     return None, None
 
 
@@ -410,7 +411,7 @@ def main():
 
     achieved = timed_bytes / args.steps / (kernel_ms * 1e-3) / 1e9 if n else 0.0
     # C5's summary: the 10M-packet pass with the bench's rewrite mask (src|dst|ports = 15)
-    traffic, traffic_src = pmc_traffic("nat15" if nat else args.workload) if args.team == 0 else (None, None)
+    traffic, traffic_src = pmc_traffic("nat15" if nat else args.workload, n) if args.team == 0 else (None, None)
     if rank == 0:
         value = total_bytes_step * args.steps / wall_max / 1e9
         kname = "k_natw (RFC 1624)" if nat else "k_csum_d (K2)"
