@@ -26,6 +26,7 @@ the cpu_baseline leg processes (the whole batch when its budget allows); every r
 sums in place and verifies them (size-independent property).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c3|c4|c5] [--strong]
+       [--share-gpu]   (more ranks than GPUs: a same-card rehearsal, reported as such)
 """
 from __future__ import annotations
 
@@ -195,8 +196,11 @@ def _free_port() -> int:
 def launch_ranks(n: int) -> int:
     """`--gpus N` without a launcher: run the N ranks as children of torch.distributed.run (this
     process has not touched the GPU) and return their exit code."""
+    argv = sys.argv[1:]
+    if "--gpus" not in argv and not any(a.startswith("--gpus=") for a in argv):
+        argv = argv + ["--gpus", str(n)]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + argv
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "1")
@@ -213,7 +217,11 @@ def launch_stats(ms: list[float]) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE under a launcher, else 1)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks share cards: a rehearsal, "
+                         "marked so in the line, never a scaling point)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
@@ -225,23 +233,27 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=6.0)
     args = ap.parse_args()
 
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    import torch   # device_count() does not initialise the GPU on this image
+    ndev = torch.cuda.device_count()
+    under_launcher = "WORLD_SIZE" in os.environ
+    world = int(os.environ.get("WORLD_SIZE", "1")) if under_launcher else (args.gpus or 1)
+    if args.gpus is not None and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch with matching counts")
+    if world > ndev and not args.share_gpu:
+        sys.exit(f"bench.py: {world} ranks but {ndev} visible GPU(s): one rank per GPU "
+                 f"(pass --share-gpu for a same-card rehearsal)")
+    if not under_launcher and world > 1:
+        sys.exit(launch_ranks(world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world:
-        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch with matching counts")
-    import torch
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    # one process per GPU; modulo the visible device count so the multi-rank path can also be
-    # rehearsed with several ranks on a single-GPU box (identity on an 8-GPU node)
-    ndev = torch.cuda.device_count()
+    # one process per GPU; with --share-gpu the ranks wrap around the visible cards (a rehearsal
+    # of the multi-rank path on a small box: devices_distinct in the line says how many cards ran)
     torch.cuda.set_device(local % max(ndev, 1))
     from vproxy_amd import vpcsum as V
-    from vproxy_amd.shard import all_ranks_ok, max_over_ranks, shard_by_bytes, sum_over_ranks
+    from vproxy_amd.shard import all_ranks_ok, gather_over_ranks, max_over_ranks, shard_by_bytes, sum_over_ranks
     V.lib()
 
     synth_id, n_cfg, stride, desc_text = WORKLOADS[args.workload]
@@ -339,6 +351,12 @@ def main():
     torch.cuda.synchronize()
     per_launch = [evs[i].elapsed_ms(evs[i + 1]) for i in range(args.steps)]
     wall_max = max_over_ranks(wall)
+    # per-rank attribution of a multi-GPU line: every rank's kernel time and the card it ran on
+    props = torch.cuda.get_device_properties(torch.cuda.current_device())
+    dev_id = str(getattr(props, "uuid", "")) or f"{props.pci_domain_id}:{props.pci_bus_id}:{props.pci_device_id}"
+    ranks_info = gather_over_ranks({"rank": rank, "device": torch.cuda.current_device(), "device_id": dev_id,
+                                    "kernel_ms": round(t_beg.elapsed_ms(t_end) / args.steps, 5),
+                                    "packets": int(n)})
     # bytes of the K timed launches (the rotation's batches differ slightly in C3's mix)
     timed_bytes = sum(batch_bytes[i % nb] for i in range(args.steps)) if not nat else bytes_per_step * args.steps
     total_bytes_step = sum_over_ranks(float(timed_bytes)) / args.steps
@@ -373,6 +391,17 @@ def main():
                 e1.record(stream)
                 pms.append(e0.elapsed_ms(e1) / 10)
             pattern_ceiling = bytes_per_step / (min(pms) * 1e-3) / 1e9
+    elif nat and n:
+        # NAT's own memory operations with no rewrite (vpcsum_nat4_pattern_probe_async: descriptor
+        # and entry reads, the header window loads, the one store of [L3+10, checksum end)),
+        # priced in the same 72 algorithmic B/packet as `achieved`
+        for _ in range(3):
+            V.nat4_pattern_probe(arena, d, rw, n, stream=stream)
+        e0.record(stream)
+        for _ in range(10):
+            V.nat4_pattern_probe(arena, d, rw, n, stream=stream)
+        e1.record(stream)
+        pattern_ceiling = bytes_per_step / (e0.elapsed_ms(e1) / 10 * 1e-3) / 1e9
 
     # correctness: (1) rank 0 against the oracle on the cpu_baseline's packets (2) every rank:
     # sums written in place, then verified on the GPU
@@ -441,6 +470,11 @@ def main():
                 "ramp_ms": round(ramp_ms, 1),
                 "ramp_launches": ramp_launches,
                 "per_launch_ms_rank0": launch_stats(per_launch) if n else None,
+                "devices_distinct": len({r["device_id"] for r in ranks_info}),
+                "shared_gpu_rehearsal": len({r["device_id"] for r in ranks_info}) < world,
+                "kernel_ms_over_ranks": {"min": min(r["kernel_ms"] for r in ranks_info),
+                                         "max": max(r["kernel_ms"] for r in ranks_info)},
+                "ranks": ranks_info if world > 1 else None,
             },
             "roofline": {
                 "bound": "hbm",
@@ -457,6 +491,10 @@ def main():
                 "measured_read_ceiling_GBps": round(read_ceiling, 1) if read_ceiling else None,
                 "measured_pattern_ceiling_GBps": round(pattern_ceiling, 1) if pattern_ceiling else None,
                 "frac_of_pattern_ceiling": round(achieved / pattern_ceiling, 4) if pattern_ceiling else None,
+                "pattern_ceiling_kernel": ("k_natw probe (same loads and stores, no rewrite)" if nat else
+                                           "k_pattern_probe (K2's chunk reads, no checksum work)")
+                if pattern_ceiling else None,
+                "traffic_over_algorithmic": round(traffic / bytes_per_step, 3) if traffic and bytes_per_step else None,
             },
             "cpu_baseline": cpu,
         }

@@ -74,6 +74,11 @@ typedef struct vpcsum_desc {
 #define VPCSUM_S_IP_OK       0x01u /* verify: stored IPv4 header checksum == recomputed   */
 #define VPCSUM_S_L4_OK       0x02u /* verify: stored L4 checksum == recomputed            */
 #define VPCSUM_S_UDP_NOCSUM  0x04u /* UDP with stored checksum 0 (RFC 768 "no checksum")  */
+#define VPCSUM_S_TTL_EXPIRED 0x20u /* NAT: VPCSUM_NAT_DEC_TTL on a TTL / hop limit <= 1 (the value
+                                    * after VPCSUM_NAT_SET_TTL when both are set): the packet is
+                                    * refused with S_BAD_DESC and nothing is written.  The reference
+                                    * never decrements such a packet: IPInputRoute drops it and
+                                    * answers ICMP time exceeded (IPInputRoute.java:81-88)      */
 #define VPCSUM_S_DONE        0x40u /* descriptor processed                                */
 #define VPCSUM_S_BAD_DESC    0x80u /* descriptor rejected (bounds/lengths); nothing written */
 
@@ -92,7 +97,8 @@ typedef struct vpcsum_desc {
 #define VPCSUM_NAT_DST      0x02u /* destination address (IPv4 16..19 / IPv6 24..39)              */
 #define VPCSUM_NAT_SPORT    0x04u /* TCP / UDP source port                                        */
 #define VPCSUM_NAT_DPORT    0x08u /* TCP / UDP destination port                                   */
-#define VPCSUM_NAT_DEC_TTL  0x10u /* IPv4 TTL / IPv6 hop limit minus 1 (after SET_TTL if both)    */
+#define VPCSUM_NAT_DEC_TTL  0x10u /* IPv4 TTL / IPv6 hop limit minus 1 (after SET_TTL if both); a
+                                   * value <= 1 refuses the packet (VPCSUM_S_TTL_EXPIRED)        */
 #define VPCSUM_NAT_SET_TTL  0x20u /* IPv4 TTL / IPv6 hop limit := the entry's ttl value           */
 
 /* IPv4-only entry, 16 bytes (BASELINE config C5: 72 algorithmic bytes per packet).
@@ -198,6 +204,13 @@ int vpcsum_read_probe_async(const uint8_t* d_buf, uint64_t bytes, uint32_t* d_si
 int vpcsum_pattern_probe_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc,
                                uint32_t n, uint32_t* d_sink, uint32_t grid, void* stream);
 
+/* NAT pattern ceiling: the memory operations of vpcsum_nat4_async (RFC 1624, wide kernel) for a
+ * rewrite of both addresses and both ports -- descriptor and entry reads, the header window loads,
+ * the one contiguous store of [L3+10, end of the L4 checksum field) -- with no rewrite: every byte
+ * is stored back unchanged.  Tooling: prices BASELINE config C5's access pattern. */
+int vpcsum_nat4_pattern_probe_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc,
+                                    const vpcsum_nat4_t* d_rw, uint32_t n, void* stream);
+
 /* Synthetic workload generator (bench / tests): deterministic counter-based splitmix64 bytes,
  * identical to oracle/csum_oracle.c:orc_synth_frame.  workload: see VPCSUM_SYNTH_*. */
 #define VPCSUM_SYNTH_C1_UDP64     1  /* IPv4/UDP L3 50 B                     */
@@ -294,6 +307,8 @@ int vpcsum_group_create_list(const int* devices, int ndev, uint64_t max_arena_by
 int vpcsum_group_destroy(vpcsum_group_t* g);
 /* page-lock once (portable: every GPU of the group maps it) */
 int vpcsum_group_register_arena(vpcsum_group_t* g, void* h_arena, uint64_t len);
+/* finish every zero-copy batch still reading the arena on each device, then unpin it */
+int vpcsum_group_unregister_arena(vpcsum_group_t* g, void* h_arena);
 /* as vpcsum_ctx_submit, capacity per GPU; h_out / h_status hold all n results in batch order */
 int vpcsum_group_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
                         uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket);

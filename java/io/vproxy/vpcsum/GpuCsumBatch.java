@@ -5,6 +5,7 @@ import io.vproxy.vpacket.AbstractIpPacket;
 import io.vproxy.vpacket.EthernetPacket;
 import io.vproxy.vpacket.IcmpPacket;
 import io.vproxy.vpacket.Ipv4Packet;
+import io.vproxy.vpacket.Ipv6Packet;
 import io.vproxy.vpxdp.ChunkInfo;
 import io.vproxy.vpxdp.XDPConsts;
 import io.vproxy.vswitch.PacketBuffer;
@@ -111,11 +112,26 @@ public final class GpuCsumBatch implements AutoCloseable {
             throw new IllegalStateException("batch full: flush first");
         }
         long l3 = frameOff + (((EthernetPacket) pkb.pkt).getVlan() >= 0 ? 18 : 14);
-        int l3len = ip.getRawPacket(AbstractIpPacket.FLAG_CHECKSUM_UNNECESSARY).length();
+        // The lengths come from the IP header fields, never from the buffer: a frame parsed with
+        // allowPartial (every XDP / tap frame, PacketBuffer.java:177 -> EthernetPacket.java:52-56)
+        // keeps its Ethernet padding in pktBuf (Ipv4Packet.initPartial does not cut it,
+        // Ipv4Packet.java:29-63) and leaves `options` empty, so getRawPacket().length() counts the
+        // padding of every 60-B frame and getHeaderSize() is 20 for any IHL.  Java's own recompute
+        // covers raw.sub(ihl*4, totalLength - ihl*4) (:55).
+        int l3len;
+        int l4off;
+        if (ip instanceof Ipv4Packet v4) {
+            l3len = v4.getTotalLength();           // Ipv4Packet.java:361
+            l4off = v4.getIhl() * 4;               // :334
+        } else {
+            Ipv6Packet v6 = (Ipv6Packet) ip;
+            l3len = 40 + v6.getPayloadLength();    // Ipv6Packet.java:332
+            l4off = v6.getHeaderSize();            // :427-435, extHeaders filled by from() (:33-35)
+        }
         long d = (long) DESC * n;
         desc.set(ValueLayout.JAVA_LONG_UNALIGNED, d, l3);
         desc.set(ValueLayout.JAVA_SHORT_UNALIGNED, d + 8, (short) l3len);
-        desc.set(ValueLayout.JAVA_SHORT_UNALIGNED, d + 10, (short) ip.getHeaderSize());
+        desc.set(ValueLayout.JAVA_SHORT_UNALIGNED, d + 10, (short) l4off);
         desc.set(ValueLayout.JAVA_BYTE, d + 12, (byte) (ip instanceof Ipv4Packet ? 4 : 6));
         desc.set(ValueLayout.JAVA_BYTE, d + 13, (byte) ip.getProtocol());
         desc.set(ValueLayout.JAVA_BYTE, d + 14, (byte) flags);
@@ -129,7 +145,9 @@ public final class GpuCsumBatch implements AutoCloseable {
     /**
      * Compute and write every deferred checksum into its frame; call at the top of
      * Iface.completeTx, before xsk.writePackets.  Returns the frames the GPU handled (0 when a
-     * small flush went back to the native path).
+     * small flush went back to the native path).  A frame whose descriptor the kernel rejected
+     * (S_BAD_DESC: nothing was written) gets its native VP_CSUM_* flags back, so the native path
+     * computes its sums at xsk.writePackets instead of the frame leaving with a stale checksum.
      */
     public int flush() throws IOException {
         if (n == 0) {
@@ -147,6 +165,10 @@ public final class GpuCsumBatch implements AutoCloseable {
         long t = VPCsum.get().submit(env, ctx, umem, umemLen, desc, n, out, status, VPCsum.MODE_WRITE);
         VPCsum.get().waitFor(env, ctx, t);
         for (int i = 0; i < n; ++i) {
+            if ((status.get(ValueLayout.JAVA_BYTE, i) & VPCsum.S_BAD_DESC) != 0) {
+                chunks[i].setCsumFlags(nativeFlagsOf[i]);
+                --done;
+            }
             chunks[i] = null;
         }
         n = 0;

@@ -47,6 +47,9 @@ public class VPCsum {
     public static final int S_UDP_NOCSUM = 0x04;
     public static final int S_DONE = 0x40;
     public static final int S_BAD_DESC = 0x80;
+    /** NAT: a TTL / hop-limit decrement of a packet at TTL <= 1 is refused (with S_BAD_DESC);
+     * IPInputRoute drops such packets and answers ICMP time exceeded (IPInputRoute.java:81-88). */
+    public static final int S_TTL_EXPIRED = 0x20;
     // modes
     public static final int MODE_COMPUTE = 0x00;
     public static final int MODE_VERIFY = 0x01;

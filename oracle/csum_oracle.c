@@ -298,6 +298,12 @@ void orc_nat_java(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, co
         return;
     }
     uint8_t* l3 = arena + off;
+    /* IPInputRoute.java:81-88: hop <= 1 is dropped (ICMP time exceeded), never decremented */
+    if ((rw->mask & VPCSUM_NAT_DEC_TTL) &&
+        ((rw->mask & VPCSUM_NAT_SET_TTL) ? rw->ttl : l3[ver == 4 ? 8 : 7]) <= 1) {
+        if (status) *status = VPCSUM_S_BAD_DESC | VPCSUM_S_TTL_EXPIRED;
+        return;
+    }
     int fld = orc_l4_field((uint32_t)proto);
     /* the L4 packet carries a checksum field (TcpPacket / UdpPacket / IcmpPacket) */
     int l4sum = fld >= 0 && !(ver == 4 && proto == 58) && len - l4o >= (uint32_t)fld + 2;

@@ -32,6 +32,7 @@ LIB_PATH = os.path.join(HERE, "build", "liborc.so")
 
 F_IP, F_L4, F_RAW, F_L4P = 0x01, 0x02, 0x04, 0x08
 S_IP_OK, S_L4_OK, S_UDP_NOCSUM, S_DONE, S_BAD_DESC = 0x01, 0x02, 0x04, 0x40, 0x80
+S_TTL_EXPIRED = 0x20
 MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
 NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL, NAT_SET_TTL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 
@@ -417,8 +418,13 @@ def nat_java_pure(l3: bytearray, ver: int, proto: int, l3_len: int, l4_off: int,
     (Ipv4Packet.setSrc/setDst/setTtl, Ipv4Packet.java:401-407, 433-458; Ipv6Packet.setSrc/setDst/
     setHopLimit, Ipv6Packet.java:354-396; TcpPacket/UdpPacket.setSrcPort/setDstPort) mark the sums
     dirty (pseudoHeaderChanges: Ipv4Packet.java:236-240, Ipv6Packet.java:238-242) and
-    getRawPacket(0) recomputes them in full.  rw: one NAT_DTYPE record."""
+    getRawPacket(0) recomputes them in full.  rw: one NAT_DTYPE record.  Returns the status:
+    S_DONE, or S_BAD_DESC | S_TTL_EXPIRED (nothing written) for a TTL decrement of a TTL / hop
+    limit <= 1, which IPInputRoute drops instead (IPInputRoute.java:81-88)."""
     m = int(rw["mask"])
+    t = 8 if ver == 4 else 7
+    if m & NAT_DEC_TTL and (int(rw["ttl"]) if m & NAT_SET_TTL else l3[t]) <= 1:
+        return S_BAD_DESC | S_TTL_EXPIRED
     fld = L4_FIELD.get(proto, -1)
     l4sum = fld >= 0 and not (ver == 4 and proto == IP_PROTOCOL_ICMPv6) and l3_len - l4_off >= fld + 2
     addr_dirty = l4sum and (proto in (IP_PROTOCOL_TCP, IP_PROTOCOL_UDP) or
@@ -432,7 +438,6 @@ def nat_java_pure(l3: bytearray, ver: int, proto: int, l3_len: int, l4_off: int,
     if m & NAT_DST:
         l3[a + alen:a + 2 * alen] = bytes(rw["dst"][:alen])
         ip_dirty, l4_dirty = ver == 4, l4_dirty or addr_dirty
-    t = 8 if ver == 4 else 7
     if m & NAT_SET_TTL:
         l3[t] = int(rw["ttl"])
         ip_dirty = ip_dirty or ver == 4
@@ -450,6 +455,7 @@ def nat_java_pure(l3: bytearray, ver: int, proto: int, l3_len: int, l4_off: int,
         l3[10:12] = ipv4_header_csum(bytes(l3), l4_off).to_bytes(2, "big")
     if l4_dirty:
         l3[l4_off + fld:l4_off + fld + 2] = l4_csum(bytes(l3), l3_len, l4_off, ver, proto).to_bytes(2, "big")
+    return S_DONE
 
 
 # ----------------------------------------------------------------------------------------

@@ -6,6 +6,9 @@ Outputs (committed, data only):
                    values that test pins (asserted or embedded in the frames it round-trips).
   pcap/*.pcap   -- the reference's pcap fixtures (test/src/test/resources/pcap/, MIT), copied
                    byte for byte as data.
+  pcap_tuples.json -- the flow tuples TestPcap.java expects of each pcap frame (PktCheck lists:
+                   src / dst address and port, and the TCP flags each PktCheck declares; the BSD
+                   loopback test's ICMP address pairs), frame by frame.
   nat.json      -- the reference's own checkPartialAndModify rewrites of the KAT frames
                    (TestPacket.java:137-181, the setSrc / setDst / setTtl / setHopLimit /
                    setSrcPort / setDstPort calls of each KAT test) and IPInputRoute's TTL decrement,
@@ -26,6 +29,8 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 
 TESTPACKET = "test/src/test/java/io/vproxy/test/cases/TestPacket.java"
+TESTPCAP = "test/src/test/java/io/vproxy/test/cases/TestPcap.java"
+CONSTS = "base/src/main/java/io/vproxy/base/util/Consts.java"
 PCAP_DIR = "test/src/test/resources/pcap"
 
 
@@ -61,7 +66,54 @@ def bytes_from_calls(body: str, var: str) -> bytes:
     raise AssertionError(var)
 
 
+def pcap_tuples(ref: str) -> dict:
+    """TestPcap.java's expectations, frame by frame: the PktCheck lists of ether() and
+    linuxCooked() (IPPort src, IPPort dst, TCP flags) and bsd()'s getSrc / getDst asserts."""
+    src = open(os.path.join(ref, TESTPCAP)).read()
+    consts = open(os.path.join(ref, CONSTS)).read()
+    tcp_flag = {m.group(1): int(m.group(2), 2)
+                for m in re.finditer(r"TCP_FLAGS_(\w+)\s*=\s*0b([01]+);", consts)}
+    assert set(tcp_flag) >= {"SYN", "ACK", "PSH", "FIN", "RST"}
+    ipport = r'new IPPort\("([^"]+)",\s*(\d+)\)'
+    out = {}
+    for meth, pcap in (("ether", "cap-ether.pcap"), ("linuxCooked", "cap-linux-cooked.pcap")):
+        body, a, b = method_body(src, meth)
+        assert f'"/pcap/{pcap}"' in body
+        addrs = {m.group(1): (m.group(2), int(m.group(3)))
+                 for m in re.finditer(r"var\s+(\w+)\s*=\s*" + ipport + ";", body)}
+        rows = []
+        line0 = a + body[:body.index("List.of(")].count("\n")
+        for m in re.finditer(r"new PktCheck\((.*?)\)(?=,\s*\n|\s*\n\s*\))", body, re.S):
+            args = m.group(1)
+            ends = []
+            for tok in re.finditer(ipport + "|" + r"\b(addr\d+)\b", args):
+                ends.append((tok.group(1), int(tok.group(2))) if tok.group(1) else addrs[tok.group(3)])
+            assert len(ends) == 2, args
+            flags = 0
+            for f in re.findall(r"Consts\.TCP_FLAGS_(\w+)", args):
+                flags |= tcp_flag[f]
+            ln = a + body[:m.start()].count("\n")
+            rows.append(dict(src=ends[0][0], sport=ends[0][1], dst=ends[1][0], dport=ends[1][1], tcp_flags=flags,
+                             source=f"{TESTPCAP}:{ln}"))
+        out[pcap] = dict(method=f"{TESTPCAP}:{a}-{b}", asserted="src/dst address and port (check(), "
+                         "TestPcap.java:16-30); tcp_flags are declared in each PktCheck but not asserted there",
+                         frames=rows)
+    body, a, b = method_body(src, "bsd")
+    pairs = {}
+    for m in re.finditer(r'assertEquals\(IP\.from\("([^"]+)"\),\s*pkts\.get\((\d+)\)\.get(Src|Dst)\(\)\)', body):
+        pairs.setdefault(int(m.group(2)), {})[m.group(3).lower()] = m.group(1)
+    assert "instanceof IcmpPacket" in body
+    out["cap-bsd-loopback-encap.pcap"] = dict(
+        method=f"{TESTPCAP}:{a}-{b}", asserted="src/dst address; every payload an IcmpPacket",
+        frames=[dict(src=pairs[i]["src"], dst=pairs[i]["dst"], proto=1) for i in sorted(pairs)])
+    assert [len(v["frames"]) for v in out.values()] == [13, 14, 4]
+    return out
+
+
 def main(ref: str) -> None:
+    with open(os.path.join(HERE, "pcap_tuples.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py (PktCheck lists parsed from TestPcap.java, TCP "
+                                "flag values from Consts.java:56-61)", "pcaps": pcap_tuples(ref)}, f, indent=1)
     src = open(os.path.join(ref, TESTPACKET)).read()
     kats = []
 

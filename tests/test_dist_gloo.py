@@ -42,7 +42,7 @@ def _free_port():
 
 def _worker(rank, world, port, q):
     import torch.distributed as dist
-    from vproxy_amd.shard import all_ranks_ok, max_over_ranks, rank_seed_first_index, shard_range
+    from vproxy_amd.shard import all_ranks_ok, gather_over_ranks, max_over_ranks, rank_seed_first_index, shard_range
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -51,7 +51,8 @@ def _worker(rank, world, port, q):
     ok = all_ranks_ok(rank != 1)
     ok_all = all_ranks_ok(True)
     lo, hi = shard_range(1000, rank, world)
-    q.put((rank, m, ok, ok_all, lo, hi, rank_seed_first_index(1 << 20, rank)))
+    g = gather_over_ranks({"rank": rank, "kernel_ms": 0.1 * (rank + 1)})
+    q.put((rank, m, ok, ok_all, lo, hi, rank_seed_first_index(1 << 20, rank), g))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -73,3 +74,27 @@ def test_gloo_world2_reductions():
     assert [r[3] for r in res] == [True, True]
     assert [(r[4], r[5]) for r in res] == [(0, 500), (500, 1000)]
     assert [r[6] for r in res] == [0, 1 << 20]               # disjoint synthetic sub-streams
+    for r in res:                                            # every rank sees every rank, in order
+        assert r[7] == [{"rank": 0, "kernel_ms": 0.1}, {"rank": 1, "kernel_ms": 0.2}]
+
+
+def _bench_cpu(args, env_extra=None):
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(repo, "bench.py")] + args, capture_output=True,
+                          text=True, timeout=120, cwd=repo, env=env)
+
+
+def test_bench_refuses_ranks_beyond_visible_gpus():
+    """bench.py never prints an N-GPU line from ranks sharing cards unless told to: here (no GPU)
+    --gpus 2 fails before launching anything, and so does a launcher's WORLD_SIZE=2 without --gpus
+    (the count is taken from the launcher)."""
+    r = _bench_cpu(["--gpus", "2", "--steps", "1"])
+    assert r.returncode != 0 and "share-gpu" in r.stderr
+    r = _bench_cpu(["--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "2 ranks but 0 visible" in r.stderr
+    r = _bench_cpu(["--gpus", "3", "--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "matching counts" in r.stderr

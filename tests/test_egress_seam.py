@@ -1,0 +1,112 @@
+"""The egress seam with frames as vproxy holds them.
+
+GpuCsumBatch.defer must describe a partially parsed frame by its IP header fields (totalLength,
+IHL, payloadLength, extension headers), not by its buffer: the buffer of a 60-B frame holds the
+Ethernet padding, and initPartial leaves IPv4 options unparsed (tests/egressvec.py).  The mirror
+(vproxy_amd/vswitch.py: egress_descriptor, EgressBatch.defer_frame) is checked here against the
+oracle's restatement of the reference parser on the CPU, and end to end on the GPU: deferred,
+flushed with in-place writes, and byte-equal to the oracle's full recompute.  A descriptor the
+kernel rejects goes back to the native path (GpuCsumBatch.flush restores the chunk's flags).
+"""
+import numpy as np
+import pytest
+
+import egressvec as E
+from oracle import oracle as O
+
+
+def _batch():
+    fs = E.frames()
+    arena, offs = E.layout(fs)
+    flags = [E.want_flags(f["ver"], f["proto"], i) for i, f in enumerate(fs)]
+    return fs, arena, offs, flags
+
+
+def test_egress_descriptor_follows_the_ip_header():
+    """egress_descriptor == the oracle parser's view for every frame (padding excluded, options
+    and extension headers skipped, L3 after an 802.1Q tag)."""
+    from vproxy_amd import vswitch as S
+    fs, arena, offs, flags = _batch()
+    want = E.oracle_descriptors(fs, offs, flags)
+    for i, (f, o) in enumerate(zip(fs, offs)):
+        d = S.egress_descriptor(arena[o:o + 64], o, flags[i])
+        assert d is not None
+        assert d.tobytes() == want[i].tobytes(), (f["kind"], d, want[i])
+
+
+def test_buffer_length_descriptors_corrupt_these_frames(orc):
+    """The round-2 derivation (buffer length, getHeaderSize) writes different bytes into the
+    frames than Java's recompute on every padded, optioned or trailer-carrying frame with an L4
+    sum to write: the vectors tell the two apart."""
+    fs, arena, offs, flags = _batch()
+    good = E.oracle_descriptors(fs, offs, flags)
+    bad = E.buffer_length_descriptors(fs, offs, flags)
+    a_good, a_bad = arena.copy(), arena.copy()
+    orc.process(a_good, good, O.MODE_COMPUTE, write=True)
+    orc.process(a_bad, bad, O.MODE_COMPUTE, write=True)
+    differs = 0
+    for i, o in enumerate(offs):
+        if flags[i] & (O.F_L4 | O.F_L4P) and good[i].tobytes() != bad[i].tobytes():
+            differs += not np.array_equal(a_good[o:o + 2048 - 384], a_bad[o:o + 2048 - 384])
+    assert differs >= 0.9 * sum(1 for i in range(len(fs)) if flags[i] & (O.F_L4 | O.F_L4P)
+                                and good[i].tobytes() != bad[i].tobytes())
+
+
+@pytest.fixture(scope="module")
+def V():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vproxy_amd import vpcsum
+    vpcsum.lib()
+    return vpcsum
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("service", [False, True])
+def test_egress_java_held_frames_on_gpu(V, orc, service):
+    """Frames deferred the way GpuCsumBatch.defer now builds descriptors, flushed once (launched,
+    or through the service grid from the registered umem), equal Java's full recompute byte for
+    byte -- padding, options and extension-header bytes untouched."""
+    from vproxy_amd import vswitch as S
+    fs, arena, offs, flags = _batch()
+    want = arena.copy()
+    orc.process(want, E.oracle_descriptors(fs, offs, flags), O.MODE_COMPUTE, write=True)
+    batch = S.EgressBatch(arena, capacity=len(fs), service_idle_us=20000 if service else 0)
+    for o, fl in zip(offs, flags):
+        assert batch.defer_frame(o, fl)
+    assert batch.complete_tx() == len(fs)
+    assert not batch.handed_back
+    assert np.array_equal(arena, want)
+    batch.close()
+
+
+@pytest.mark.gpu
+def test_egress_rejected_descriptor_is_handed_back(V, orc):
+    """A frame the kernel refuses (a TCP segment too short to hold its checksum field) is not
+    written and is handed back, the others are written; the flush reports only the GPU's frames."""
+    from vproxy_amd import vswitch as S
+    fs, arena, offs, flags = _batch()
+    fs, offs, flags = fs[:40], offs[:40], flags[:40]
+    arena = arena[:40 * E.CHUNK].copy()
+    # frame 7 becomes IPv4/TCP with totalLength 30: 10 B of TCP, no room for the field at +16
+    o = offs[7]
+    hl = 18 if fs[7]["vlan"] else 14
+    arena[o + hl] = 0x45
+    arena[o + hl + 9] = 6
+    arena[o + hl + 2:o + hl + 4] = [0, 30]
+    flags[7] = O.F_IP | O.F_L4
+    before7 = arena[o:o + 128].copy()
+    good = [i for i in range(40) if i != 7]
+    want = arena.copy()
+    d_all = E.oracle_descriptors([fs[i] for i in good], [offs[i] for i in good], [flags[i] for i in good])
+    orc.process(want, d_all, O.MODE_COMPUTE, write=True)
+    batch = S.EgressBatch(arena, capacity=64)
+    for oo, fl in zip(offs, flags):
+        batch.defer_frame(oo, fl)
+    assert batch.complete_tx() == 39
+    assert batch.stats["rejected"] == 1
+    assert len(batch.handed_back) == 1 and int(batch.handed_back[0][0]["l3_off"]) == o + hl
+    assert np.array_equal(arena[o:o + 128], before7)
+    assert np.array_equal(arena, want)
+    batch.close()

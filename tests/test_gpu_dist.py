@@ -19,12 +19,20 @@ def _bench(*args):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-           "--ramp-ms", "0", "--no-cpu-baseline"] + list(args)
+           "--ramp-ms", "0", "--no-cpu-baseline", "--share-gpu"] + list(args)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout   # rank 0 alone prints
-    return json.loads(lines[0])
+    j = json.loads(lines[0])
+    c = j["config"]
+    # two ranks on this box's one card: the line says so, and names each rank's kernel time
+    ndev = torch.cuda.device_count()
+    assert c["devices_distinct"] == min(2, ndev)
+    assert c["shared_gpu_rehearsal"] is (ndev < 2)
+    assert [r["rank"] for r in c["ranks"]] == [0, 1]
+    assert c["kernel_ms_over_ranks"]["min"] <= c["kernel_ms_over_ranks"]["max"]
+    return j
 
 
 @pytest.mark.parametrize("workload", ["c2", "c3", "c1"])
@@ -53,6 +61,18 @@ def test_bench_two_ranks_strong(workload):
     assert c["packets_rank0"] < c["global_batch"]
     assert abs(c["algorithmic_bytes_per_step_all_ranks"] - 2 * c["algorithmic_bytes_per_step_rank0"]) \
         < 0.01 * c["algorithmic_bytes_per_step_all_ranks"]
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """Without --share-gpu, more ranks than visible cards is an error (no "N-GPU" line from ranks
+    sharing one card)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n = torch.cuda.device_count() + 1
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, cwd=REPO)
+    assert r.returncode != 0 and "share-gpu" in r.stderr
 
 
 @pytest.mark.parametrize("ndev", [1, 3])

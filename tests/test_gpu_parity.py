@@ -258,15 +258,18 @@ def test_nat_wide_and_scalar_kernels(V, orc, pad, workload, packed):
     n = 1500 if workload == O.SYNTH_FUZZ else 3000
     arena, desc, rw = _nat_batch(orc, n, seed=pad + 17, udp_zero=0.1, pad=pad, workload=workload, packed=packed)
     want = arena.copy()
-    orc.nat4_java(want, desc, rw)
+    want_st = orc.nat4_java(want, desc, rw)
+    v4 = desc["l3_ver"] == 4
+    assert np.all(want_st[~v4] == O.S_BAD_DESC)
+    assert set(np.unique(want_st[v4])) <= {O.S_DONE, O.S_BAD_DESC | O.S_TTL_EXPIRED}
     # default, byte-access kernel (bit 8), wide kernel with 1 / 2 / 4 packets per lane (bits 12..14)
     for force_scalar in (0, 0x100, 0x1000, 0x2000, 0x3000):
         got, st = _gpu_nat(V, arena, desc, rw, V.NAT_RFC1624 | force_scalar)
-        v4 = desc["l3_ver"] == 4
-        assert np.all(st[v4] == O.S_DONE) and np.all(st[~v4] == O.S_BAD_DESC)
+        assert np.array_equal(st, want_st), force_scalar
         assert np.array_equal(got, want), force_scalar
-        got, _ = _gpu_nat(V, arena, desc, rw, V.NAT_STRICT_JAVA | force_scalar)
+        got, st = _gpu_nat(V, arena, desc, rw, V.NAT_STRICT_JAVA | force_scalar)
         assert np.array_equal(got, want), force_scalar
+        assert np.array_equal(st & (O.S_BAD_DESC | O.S_TTL_EXPIRED), want_st & (O.S_BAD_DESC | O.S_TTL_EXPIRED))
 
 
 def _gpu_nat(V, arena_np, desc, rw, mode):
@@ -281,9 +284,9 @@ def _gpu_nat(V, arena_np, desc, rw, mode):
 def test_nat_rfc1624_bit_exact_on_valid_input(V, orc):
     arena, desc, rw = _nat_batch(orc, 4000, udp_zero=0.1)
     want = arena.copy()
-    orc.nat4_java(want, desc, rw)
+    want_st = orc.nat4_java(want, desc, rw)
     got, st = _gpu_nat(V, arena, desc, rw, V.NAT_RFC1624)
-    assert np.all(st == O.S_DONE)
+    assert np.array_equal(st, want_st)
     assert np.array_equal(got, want)
 
 
@@ -367,11 +370,11 @@ def test_nat_v4_v6_against_java(V, orc, pad):
     rng = np.random.default_rng(100 + pad)
     arena, desc, rw = _nat48_batch(orc, rng, 1500, pad)
     want = arena.copy()
-    orc.nat_java(want, desc, rw)
+    want_st = orc.nat_java(want, desc, rw)
     for mode in (V.NAT_RFC1624, V.NAT_STRICT_JAVA, V.NAT_RFC1624 | 0x100, V.NAT_STRICT_JAVA | 0x100,
                  V.NAT_RFC1624 | 0x1000, V.NAT_RFC1624 | 0x3000):
         got, st = _gpu_nat48(V, arena, desc, rw, mode)
-        assert np.all(st == O.S_DONE), hex(mode)
+        assert np.array_equal(st, want_st), hex(mode)
         assert np.array_equal(got, want), hex(mode)
     # corrupted inputs: strict Java still matches, RFC 1624 diverges exactly there
     arena, desc, rw = _nat48_batch(orc, rng, 800, pad, corrupt=0.3)
@@ -1100,7 +1103,7 @@ def test_nat_arena_beyond_4gib(V, orc):
     arena, desc, rw = _nat48_batch(orc, rng, 600, 6)
     n, stride = len(desc), 9088
     want = arena.copy()
-    orc.nat_java(want, desc, rw)
+    want_st = orc.nat_java(want, desc, rw)
     big = torch.zeros((5 << 30) + 4096, dtype=torch.uint8, device="cuda")
     bases = np.sort(rng.choice(((5 << 30) - (1 << 20)) // 16384, n, replace=False)) * 16384 + 8
     bases[: n // 3] = np.arange(n // 3) * 16384 + 8
@@ -1113,7 +1116,7 @@ def test_nat_arena_beyond_4gib(V, orc):
     st = torch.zeros(n, dtype=torch.uint8, device="cuda")
     V.nat(big, V.desc_to_tensor(dg), dev(rw.view(np.uint8)), n, st, V.NAT_RFC1624)
     torch.cuda.synchronize()
-    assert np.all(st.cpu().numpy() == O.S_DONE)
+    assert np.array_equal(st.cpu().numpy(), want_st)
     for i in rng.choice(n, 100, replace=False):
         got = big[int(bases[i]): int(bases[i]) + stride].cpu().numpy()
         assert np.array_equal(got, want[i * stride:(i + 1) * stride]), i
@@ -1214,3 +1217,80 @@ def test_ctx_parse_frames_tuples(V, orc):
     want, want_st = orc.process(arena, good, O.MODE_VERIFY)
     ctx.close()
     assert np.array_equal(vout, want) and np.array_equal(vst, want_st)
+
+
+@pytest.mark.parametrize("mode", [0, 0x100, 1, 0x101])   # RFC 1624 / strict Java, wide / byte kernel
+def test_nat_ttl_expired_on_gpu(V, orc, mode):
+    """TTL / hop limit 0 and 1 under NAT_DEC_TTL (alone, after SET_TTL, with an address rewrite):
+    refused with S_BAD_DESC | S_TTL_EXPIRED, nothing written; TTL 2 and 64 decremented.  Both
+    entry formats, IPv4 and IPv6, every kernel and mode; statuses and bytes equal the oracle's."""
+    rng = np.random.default_rng(77)
+    arena, desc = orc.synth(400, 9088, 2, O.SYNTH_FUZZ, O.SEED, 6060)
+    rw = np.zeros(len(desc), O.NAT_DTYPE)
+    rw.view(np.uint8).reshape(-1, 48)[:, :36] = rng.integers(0, 256, (len(desc), 36), dtype=np.uint8)
+    for i, d in enumerate(desc):
+        t = int(d["l3_off"]) + (8 if d["l3_ver"] == 4 else 7)
+        arena[t] = [0, 1, 2, 64][i % 4]
+        rw[i]["mask"] = O.NAT_DEC_TTL | [0, O.NAT_SET_TTL, O.NAT_SRC | O.NAT_DPORT][(i // 4) % 3]
+        rw[i]["ttl"] = [0, 1, 2, 9][(i // 12) % 4]
+    orc.process(arena, desc, O.MODE_COMPUTE, write=True)
+    want = arena.copy()
+    want_st = orc.nat_java(want, desc, rw)
+    assert (want_st == (O.S_BAD_DESC | O.S_TTL_EXPIRED)).sum() > 100 and (want_st == O.S_DONE).sum() > 100
+    got, st = _gpu_nat48(V, arena, desc, rw, mode)
+    assert np.array_equal(st, want_st)
+    assert np.array_equal(got, want)
+    v4 = desc["l3_ver"] == 4
+    want4 = arena.copy()
+    want4_st = orc.nat4_java(want4, desc[v4], _nat4_of(rw[v4]))
+    got4, st4 = _gpu_nat(V, arena, desc[v4], _nat4_of(rw[v4]), mode)
+    assert np.array_equal(st4, want4_st) and np.array_equal(got4, want4)
+
+
+def test_library_restores_callers_device(V, orc):
+    """Every context / group entry point runs on its own device and gives the caller's current
+    device back (api.cpp DeviceScope): torch's current device is unchanged after create, register,
+    submit, wait, service, NAT and destroy.  With two or more GPUs the contexts live on device 1
+    while the caller sits on device 0; on a one-GPU box the group is [0, 0] (the save / restore
+    path runs, the device cannot differ)."""
+    import torch
+    ndev = torch.cuda.device_count()
+    other = 1 if ndev > 1 else 0
+    torch.cuda.set_device(0)
+    arena, desc = orc.synth(64, 2048, 14, O.SYNTH_C3, O.SEED, 808)
+    want, _ = orc.process(arena, desc)
+    g = V.Group([other, 0], max_arena=arena.nbytes, max_pkts=64)
+    assert torch.cuda.current_device() == 0
+    g.register(arena)
+    out, _ = g.run(arena, desc)
+    assert np.array_equal(out, want) and torch.cuda.current_device() == 0
+    g.unregister(arena)
+    out, _ = g.run(arena, desc)
+    assert np.array_equal(out, want) and torch.cuda.current_device() == 0
+    g.close()
+    ctx = V.Context(other, max_arena=arena.nbytes, max_pkts=64)
+    ctx.register(arena)
+    ctx.set_service(20000)
+    out, _ = ctx.run(arena, desc)
+    assert np.array_equal(out, want) and torch.cuda.current_device() == 0
+    ctx.close()
+    assert torch.cuda.current_device() == 0
+
+
+def test_group_register_unregister_cycle(V, orc):
+    """vpcsum_group_unregister_arena: the arena can be registered again afterwards (the page-lock
+    was released), batches run zero-copy while registered and staged after; unregistering an arena
+    the group does not hold is an error."""
+    arena, desc = orc.synth(200, 2048, 14, O.SYNTH_C3, O.SEED, 909)
+    want, _ = orc.process(arena, desc)
+    g = V.Group([0, 0], max_arena=arena.nbytes, max_pkts=256)
+    for _ in range(3):
+        g.register(arena)
+        out, _ = g.run(arena, desc)
+        assert np.array_equal(out, want)
+        g.unregister(arena)
+    with pytest.raises(V.VpcsumError, match="not registered"):
+        g.unregister(arena)
+    out, _ = g.run(arena, desc)
+    assert np.array_equal(out, want)
+    g.close()

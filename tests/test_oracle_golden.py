@@ -275,14 +275,47 @@ def test_nat_pure_vs_c_random(orc):
     rw["mask"] = rng.integers(0, 64, n)
     want = arena.copy()
     st = orc.nat_java(want, desc, rw)
-    assert np.all(st == O.S_DONE)
+    assert set(np.unique(st)) <= {O.S_DONE, O.S_BAD_DESC | O.S_TTL_EXPIRED}
     got = arena.copy()
-    for d, r in zip(desc, rw):
+    for i, (d, r) in enumerate(zip(desc, rw)):
         o, L = int(d["l3_off"]), int(d["l3_len"])
         l3 = bytearray(got[o:o + L].tobytes())
-        O.nat_java_pure(l3, int(d["l3_ver"]), int(d["l4_proto"]), L, int(d["l4_off"]), r)
+        assert O.nat_java_pure(l3, int(d["l3_ver"]), int(d["l4_proto"]), L, int(d["l4_off"]), r) == st[i]
         got[o:o + L] = np.frombuffer(bytes(l3), np.uint8)
     assert np.array_equal(got, want)
+
+
+def test_nat_ttl_expired_refused(orc):
+    """A TTL / hop-limit decrement of a packet at TTL <= 1 (after SET_TTL when both are asked) is
+    refused with S_BAD_DESC | S_TTL_EXPIRED and the packet left as it was: the reference never
+    decrements it (IPInputRoute.java:81-88 drops it and answers ICMP time exceeded).  TTL 2
+    decrements to 1 as setTtl(ttl - 1) does."""
+    arena, desc = orc.synth(24, 2048, 14, O.SYNTH_FUZZ, O.SEED, 5150)
+    orc.process(arena, desc, O.MODE_COMPUTE, write=True)
+    rw = np.zeros(len(desc), O.NAT_DTYPE)
+    cases = []   # (stored ttl, mask, entry ttl, expired)
+    for i, d in enumerate(desc):
+        ttl = [0, 1, 2, 64][i % 4]
+        k = (i // 4) % 3
+        mask, ettl = [(O.NAT_DEC_TTL, 0), (O.NAT_DEC_TTL | O.NAT_SET_TTL, ttl), (O.NAT_DEC_TTL | O.NAT_SRC, 0)][k]
+        if k == 1:
+            arena[int(d["l3_off"]) + (8 if d["l3_ver"] == 4 else 7)] = 200   # SET_TTL decides, not the stored value
+        else:
+            arena[int(d["l3_off"]) + (8 if d["l3_ver"] == 4 else 7)] = ttl
+        rw[i]["mask"], rw[i]["ttl"] = mask, ettl
+        cases.append(ttl <= 1)
+    orc.process(arena, desc, O.MODE_COMPUTE, write=True)
+    want = arena.copy()
+    st = orc.nat_java(want, desc, rw)
+    for i, d in enumerate(desc):
+        o, L = int(d["l3_off"]), int(d["l3_len"])
+        if cases[i]:
+            assert st[i] == O.S_BAD_DESC | O.S_TTL_EXPIRED
+            assert np.array_equal(want[o:o + L], arena[o:o + L])
+        else:
+            assert st[i] == O.S_DONE
+            t = 8 if d["l3_ver"] == 4 else 7
+            assert want[o + t] == (int(rw[i]["ttl"]) if rw[i]["mask"] & O.NAT_SET_TTL else arena[o + t]) - 1
 
 
 def test_flow_tuple_pinned():

@@ -12,6 +12,7 @@ ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--nat", type=int, default=-1, help="nat_mode: profile vpcsum_nat4_async on C5 instead")
 ap.add_argument("--nat-mask", type=int, default=0x0F, help="rewrite mask of every entry (0: read-only pass)")
 ap.add_argument("--nat-n", type=int, default=10_000_000, help="C5 packets (BASELINE: 10M)")
+ap.add_argument("--nat-probe", action="store_true", help="the NAT pattern probe (same memory operations, no rewrite)")
 a = ap.parse_args()
 if a.nat >= 0:
     n, stride = a.nat_n, 2048
@@ -26,7 +27,10 @@ if a.nat >= 0:
     rw = rw.cuda()
     st = torch.zeros(n, dtype=torch.uint8, device="cuda")
     for _ in range(a.iters):
-        V.nat4(arena, d, rw, n, st, a.nat)
+        if a.nat_probe:
+            V.nat4_pattern_probe(arena, d, rw, n)
+        else:
+            V.nat4(arena, d, rw, n, st, a.nat)
     torch.cuda.synchronize()
     print("done")
     sys.exit(0)

@@ -47,6 +47,27 @@ static int hipfail(hipError_t e, const char* what) {
         if (e__ != hipSuccess) return hipfail(e__, what); \
     } while (0)
 
+// Makes `device` current for one entry point and gives the caller its own current device back on
+// every exit path: a torch or Java caller working on another device never sees it change.
+struct DeviceScope {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceScope(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != device) err = hipSetDevice(device);
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
+#define VPC_ON_DEVICE(dev)                                                      \
+    DeviceScope dscope__(dev);                                                  \
+    if (dscope__.err != hipSuccess) return hipfail(dscope__.err, "hipSetDevice")
+
 int num_cus(int device) {
     static std::mutex mu;
     static std::vector<int> cache;
@@ -214,6 +235,8 @@ static int nat_run(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_
         VPC_CHECK(launch_csum(d_arena, arena_len, d_desc, n, nullptr, d_status, d_status, VPCSUM_MODE_WRITE, d_arena,
                               0, 0, s),
                   "nat recompute launch");
+        // pass 3: the TTL-expired packets (refused, untouched) get S_TTL_EXPIRED next to S_BAD_DESC
+        VPC_CHECK(launch_nat_ttl_status(d_arena, arena_len, d_desc, d_rw, fmt, n, d_status, s), "nat ttl status launch");
         return 0;
     }
     VPC_CHECK(launch_nat(d_arena, arena_len, d_desc, d_rw, fmt, n, d_status, nullptr, nat_mode, s), "nat launch");
@@ -229,6 +252,15 @@ static int nat_async(const char* what, uint8_t* d_arena, uint64_t arena_len, con
     if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u | 0x7000u)) return fail("%s: bad nat_mode 0x%x", what, nat_mode);
     if ((nat_mode & VPCSUM_NAT_STRICT_JAVA) && !d_status) return fail("%s: strict-java mode needs a status buffer", what);
     return nat_run(d_arena, arena_len, d_desc, d_rw, fmt, n, d_status, nat_mode, (hipStream_t)stream);
+}
+
+int vpcsum_nat4_pattern_probe_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc,
+                                    const vpcsum_nat4_t* d_rw, uint32_t n, void* stream) {
+    if (n == 0) return 0;
+    if (!d_arena || !d_desc || !d_rw) return fail("vpcsum_nat4_pattern_probe_async: NULL argument");
+    VPC_CHECK(launch_nat_probe(d_arena, arena_len, d_desc, d_rw, 0, n, (hipStream_t)stream),
+              "vpcsum_nat4_pattern_probe_async launch");
+    return 0;
 }
 
 int vpcsum_nat4_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const vpcsum_nat4_t* d_rw,
@@ -364,7 +396,7 @@ static void svc_free(vpcsum_ctx* c) {
 int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
     if (!c) return fail("vpcsum_ctx_set_service: NULL context");
     std::lock_guard<std::mutex> lk(c->mu);
-    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    VPC_ON_DEVICE(c->device);
     for (auto& s : c->slots)
         if (s.busy && slot_finish(c, s) != 0) return -1;
     svc_free(c);
@@ -411,7 +443,7 @@ int vpcsum_ctx_stats(vpcsum_ctx_t* c, uint64_t* service_batches, uint64_t* servi
 int vpcsum_ctx_create(int device, uint64_t max_arena_bytes, uint32_t max_pkts, vpcsum_ctx_t** out) {
     if (!out) return fail("vpcsum_ctx_create: out is NULL");
     if (max_arena_bytes == 0 || max_pkts == 0) return fail("vpcsum_ctx_create: zero capacity");
-    VPC_CHECK(hipSetDevice(device), "hipSetDevice");
+    VPC_ON_DEVICE(device);
     vpcsum_ctx* c = new vpcsum_ctx();
     c->device = device;
     c->max_arena = max_arena_bytes;
@@ -446,7 +478,7 @@ int vpcsum_ctx_create(int device, uint64_t max_arena_bytes, uint32_t max_pkts, v
 
 int vpcsum_ctx_destroy(vpcsum_ctx_t* c) {
     if (!c) return 0;
-    (void)hipSetDevice(c->device);
+    DeviceScope on_dev(c->device);
     svc_free(c);
     for (auto& s : c->slots) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
@@ -461,7 +493,7 @@ int vpcsum_ctx_destroy(vpcsum_ctx_t* c) {
 int vpcsum_ctx_register_arena(vpcsum_ctx_t* c, void* h_arena, uint64_t len) {
     if (!c || !h_arena || len == 0) return fail("vpcsum_ctx_register_arena: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
-    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    VPC_ON_DEVICE(c->device);
     VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterMapped), "hipHostRegister");
     void* dev = nullptr;
     hipError_t e = hipHostGetDevicePointer(&dev, h_arena, 0);
@@ -476,7 +508,7 @@ int vpcsum_ctx_register_arena(vpcsum_ctx_t* c, void* h_arena, uint64_t len) {
 int vpcsum_ctx_unregister_arena(vpcsum_ctx_t* c, void* h_arena) {
     if (!c || !h_arena) return fail("vpcsum_ctx_unregister_arena: bad argument");
     std::lock_guard<std::mutex> lk(c->mu);
-    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    VPC_ON_DEVICE(c->device);
     for (size_t i = 0; i < c->registered.size(); ++i) {
         if (c->registered[i].host == (uint8_t*)h_arena) {
             // a zero-copy batch (launched or on the service grid) may still read and write the
@@ -637,7 +669,7 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
     if (n && (!h_arena || !h_desc)) return fail("vpcsum_ctx_submit: NULL arena or descriptors");
     if (mode & ~(VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_ctx_submit: bad mode 0x%x", mode);
     std::lock_guard<std::mutex> lk(c->mu);
-    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    VPC_ON_DEVICE(c->device);
     const uint64_t t = c->next_ticket++;
     Slot& s = c->slots[t & 1];
     if (s.busy && slot_finish(c, s) != 0) return -1;
@@ -792,7 +824,7 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
 int vpcsum_ctx_wait(vpcsum_ctx_t* c, uint64_t ticket) {
     if (!c) return fail("vpcsum_ctx_wait: NULL context");
     std::lock_guard<std::mutex> lk(c->mu);
-    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    VPC_ON_DEVICE(c->device);
     Slot& s = c->slots[ticket & 1];
     if (!s.busy || s.ticket != ticket) {
         if (ticket == 0 || ticket >= c->next_ticket) return fail("vpcsum_ctx_wait: unknown ticket %llu", (unsigned long long)ticket);
@@ -809,7 +841,7 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
     if (n && (!h_arena || !h_frame_off || !h_frame_len || !h_status))
         return fail("vpcsum_ctx_verify_frames: NULL arena, frame table or status");
     std::lock_guard<std::mutex> lk(c->mu);
-    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    VPC_ON_DEVICE(c->device);
     uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
     if (n && !base) return fail("vpcsum_ctx_verify_frames: the arena must be registered (vpcsum_ctx_register_arena)");
     const uint64_t t = c->next_ticket++;
@@ -849,7 +881,7 @@ int vpcsum_ctx_parse_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t ar
     if (n > c->max_pkts) return fail("vpcsum_ctx_parse_frames: %u frames > capacity %u", n, c->max_pkts);
     if (n && (!h_arena || !h_frame_off || !h_frame_len)) return fail("vpcsum_ctx_parse_frames: NULL arena or frame table");
     std::lock_guard<std::mutex> lk(c->mu);
-    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    VPC_ON_DEVICE(c->device);
     uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
     if (n && !base) return fail("vpcsum_ctx_parse_frames: the arena must be registered (vpcsum_ctx_register_arena)");
     const uint64_t t = c->next_ticket++;
@@ -898,7 +930,7 @@ int vpcsum_ctx_nat_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len,
     if (n && (!h_arena || !h_desc || !h_rw)) return fail("vpcsum_ctx_nat_submit: NULL arena, descriptors or rewrites");
     if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u)) return fail("vpcsum_ctx_nat_submit: bad nat_mode 0x%x", nat_mode);
     std::lock_guard<std::mutex> lk(c->mu);
-    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    VPC_ON_DEVICE(c->device);
     const uint64_t t = c->next_ticket++;
     Slot& s = c->slots[t & 1];
     if (s.busy && slot_finish(c, s) != 0) return -1;
@@ -980,7 +1012,7 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint
     if (copy_bytes > stride) return fail("vpcsum_ctx_pipeline: copy_bytes > stride");
     if (mode & ~(VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_ctx_pipeline: bad mode");
     std::lock_guard<std::mutex> lk(c->mu);
-    VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    VPC_ON_DEVICE(c->device);
     for (auto& s : c->slots)
         if (s.busy && slot_finish(c, s) != 0) return -1;
     const uint32_t per = (n + chunks - 1) / chunks;
@@ -1114,16 +1146,47 @@ int vpcsum_group_destroy(vpcsum_group_t* g) {
 int vpcsum_group_register_arena(vpcsum_group_t* g, void* h_arena, uint64_t len) {
     if (!g || !h_arena || len == 0) return fail("vpcsum_group_register_arena: bad argument");
     std::lock_guard<std::mutex> lk(g->mu);
-    VPC_CHECK(hipSetDevice(g->ctx[0]->device), "hipSetDevice");
+    VPC_ON_DEVICE(g->ctx[0]->device);
     VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterMapped | hipHostRegisterPortable), "hipHostRegister");
-    g->reg.push_back((uint8_t*)h_arena);
-    for (auto* c : g->ctx) {
+    for (size_t i = 0; i < g->ctx.size(); ++i) {
+        vpcsum_ctx* c = g->ctx[i];
         std::lock_guard<std::mutex> lc(c->mu);
+        DeviceScope on_dev(c->device);
         void* dev = nullptr;
-        VPC_CHECK(hipSetDevice(c->device), "hipSetDevice");
-        VPC_CHECK(hipHostGetDevicePointer(&dev, h_arena, 0), "hipHostGetDevicePointer");
+        hipError_t e = on_dev.err;
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&dev, h_arena, 0);
+        if (e != hipSuccess) {
+            // roll back: no context keeps a mapping of an arena the group failed to register, so
+            // a retry starts from scratch
+            for (size_t q = 0; q < i; ++q) {
+                std::lock_guard<std::mutex> lq(g->ctx[q]->mu);
+                auto& rq = g->ctx[q]->registered;
+                for (size_t k = rq.size(); k-- > 0;)
+                    if (rq[k].host == (uint8_t*)h_arena && !rq[k].owned) rq.erase(rq.begin() + k);
+            }
+            (void)hipHostUnregister(h_arena);
+            return hipfail(e, "vpcsum_group_register_arena: device mapping");
+        }
         c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, false});
     }
+    g->reg.push_back((uint8_t*)h_arena);
+    return 0;
+}
+
+int vpcsum_group_unregister_arena(vpcsum_group_t* g, void* h_arena) {
+    if (!g || !h_arena) return fail("vpcsum_group_unregister_arena: bad argument");
+    std::lock_guard<std::mutex> lk(g->mu);
+    auto it = std::find(g->reg.begin(), g->reg.end(), (uint8_t*)h_arena);
+    if (it == g->reg.end()) return fail("vpcsum_group_unregister_arena: arena not registered");
+    // every context finishes its zero-copy batches on the arena and forgets the mapping
+    // (vpcsum_ctx_unregister_arena; the contexts do not own the page-lock), then the group unpins it
+    int rc = 0;
+    for (auto* c : g->ctx)
+        if (vpcsum_ctx_unregister_arena(c, h_arena) != 0) rc = -1;
+    if (rc != 0) return -1;
+    g->reg.erase(it);
+    VPC_ON_DEVICE(g->ctx[0]->device);
+    VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
     return 0;
 }
 

@@ -45,6 +45,12 @@ hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint
 // VPCSUM_NAT_STRICT_JAVA the kernel only rewrites and stores Java's dirty flags in flags_out.
 hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw, int fmt,
                       uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream);
+// NAT's memory operations without the rewrite (tooling: the C5 pattern ceiling)
+hipError_t launch_nat_probe(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw, int fmt,
+                            uint32_t n, hipStream_t stream);
+// strict mode, after the recompute: S_TTL_EXPIRED on the packets refused for their TTL
+hipError_t launch_nat_ttl_status(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw,
+                                 int fmt, uint32_t n, uint8_t* status, hipStream_t stream);
 
 hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const uint64_t* frame_off,
                               const uint32_t* frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* desc,

@@ -137,6 +137,16 @@ __device__ __forceinline__ NatAcc nat_setters(uint8_t* w, int ver, int proto, in
     return a;
 }
 
+// IPInputRoute.java:81-88: a packet whose TTL / hop limit is <= 1 is dropped (and answered with
+// ICMP time exceeded), never decremented: DEC_TTL refuses it -- nothing written -- rather than
+// storing 0 or 255.  The value checked is the one DEC_TTL would decrement (after SET_TTL).
+__device__ __forceinline__ bool nat_ttl_expired(const uint8_t* l3, int ver, const NatRw& r) {
+    if (!(r.mask & VPCSUM_NAT_DEC_TTL)) return false;
+    const int t = (r.mask & VPCSUM_NAT_SET_TTL) ? r.ttl : (int)l3[ver == 4 ? 8 : 7];
+    return t <= 1;
+}
+constexpr uint32_t kNatExpired = VPCSUM_S_BAD_DESC | VPCSUM_S_TTL_EXPIRED;
+
 // RFC 1624 eqn. 3 on the fields of w.  Returns true when the L4 sum is a UDP "no checksum" (stored
 // 0): Java recomputes it in full (UdpPacket.java:136-164), done by nat_udp_full once the rewritten
 // header is in memory.
@@ -218,6 +228,7 @@ __device__ uint32_t nat_scalar(uint8_t* __restrict__ arena, uint64_t arena_len, 
     const int ver = dv.w & 0xff, proto = (dv.w >> 8) & 0xff;
     if (!nat_desc_ok(off, len, l4o, ver, arena_len, FMT)) return strict ? kFlagRejected : VPCSUM_S_BAD_DESC;
     uint8_t* l3 = arena + off;
+    if (nat_ttl_expired(l3, ver, r)) return strict ? kFlagRejected : kNatExpired;
     const bool l4sum = nat_l4sum(ver, proto, len, l4o);
     NatAcc a = nat_setters(l3, ver, proto, len, l4o, l4sum, r);
     if (strict) return (a.ip_dirty ? VPCSUM_F_IP : 0) | (a.l4_dirty ? VPCSUM_F_L4 : 0);
@@ -265,9 +276,46 @@ __global__ __launch_bounds__(256) void k_nat(uint8_t* __restrict__ arena, uint64
 // stores (bytewise only where it would pass the packet end: the next bytes may be another
 // packet's).  W packets per lane and iteration keep W windows in flight.
 constexpr int kNatChunks = 6;                   // window: 96 B
+
+// Store back bytes [lo, hi) of the packet (relative to L3; the window holds it at w + r0, base is
+// the window's 16-B aligned global address) as one run of dwords, widest first, bytewise only
+// where a dword would pass the packet end (the next bytes may be another packet's).
+__device__ __forceinline__ void nat_store_range(uint8_t* base, const uint32_t* slot, const uint8_t* w, int r0,
+                                                int len, int lo, int hi) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(1))) uint32_t g32;
+    if (hi <= lo) return;
+    const int lim = r0 + len;
+    int j = (r0 + lo) >> 2;
+    const int je = (r0 + hi + 3) >> 2;
+    const int jfull = lim >> 2;   // dwords below this lie inside the packet
+    while (j < je) {
+        uint8_t* dst = base + 4 * j;
+        if (!(j & 3) && j + 4 <= je && j + 4 <= jfull) {
+            const v4u q = {slot[j], slot[j + 1], slot[j + 2], slot[j + 3]};
+            *(__attribute__((address_space(1))) v4u*)dst = q;
+            j += 4;
+        } else if (!(j & 1) && j + 2 <= je && j + 2 <= jfull) {
+            const v2u q = {slot[j], slot[j + 1]};
+            *(__attribute__((address_space(1))) v2u*)dst = q;
+            j += 2;
+        } else if (j + 1 <= jfull) {
+            *(g32*)dst = slot[j];
+            j += 1;
+        } else {
+            for (int q = 4 * j; q < lim; ++q) base[q] = w[q];
+            j += 1;
+        }
+    }
+}
 constexpr int kNatSlotDw = 4 * kNatChunks + 1;  // LDS slot per lane: an odd dword stride (no bank conflicts)
 
-template <int FMT, bool STRICT, int W>
+// PROBE: the same loads, LDS staging and stores with no rewrite -- the changed range is set to
+// what a rewrite of both addresses and ports produces ([10, L4 checksum end) for IPv4, [8, ..) for
+// IPv6) and the window is stored back unchanged.  It prices NAT's access pattern (the "pattern
+// ceiling" of BASELINE config C5): a rewrite cannot run faster than its own memory operations.
+template <int FMT, bool STRICT, int W, bool PROBE = false>
 __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint64_t arena_len,
                                              const uint4* __restrict__ desc, const void* __restrict__ rw, uint32_t n,
                                              uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out) {
@@ -319,7 +367,7 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
             res[i] = 0;
             if (p >= n) continue;
             if (!wend[i]) {
-                res[i] = nat_scalar<FMT>(arena, arena_len, dv[i], rr[i], STRICT);
+                if (!PROBE) res[i] = nat_scalar<FMT>(arena, arena_len, dv[i], rr[i], STRICT);
                 continue;
             }
             const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
@@ -336,35 +384,20 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
                 }
             }
             uint8_t* l3w = w + r0;
+            if (PROBE) {
+                int hi = ver == 4 ? 20 : 40;
+                if (nat_l4sum(ver, proto, len, l4o)) hi = max(hi, l4o + l4_field(proto) + 2);
+                nat_store_range(base, slot, w, r0, len, ver == 4 ? 10 : 8, hi);
+                res[i] = VPCSUM_S_DONE;
+                continue;
+            }
+            if (nat_ttl_expired(l3w, ver, rr[i])) {
+                res[i] = STRICT ? kFlagRejected : kNatExpired;
+                continue;
+            }
             NatAcc a = nat_setters(l3w, ver, proto, len, l4o, nat_l4sum(ver, proto, len, l4o), rr[i]);
             const bool udp_zero = !STRICT && nat_rfc1624(l3w, proto, l4o, l4_field(proto), a);
-            // store back [lo, hi) of the packet as one run of dwords, widest first
-            if (a.hi > a.lo) {
-                const int lim = r0 + len;
-                int j = (r0 + a.lo) >> 2;
-                const int je = (r0 + a.hi + 3) >> 2;
-                const int jfull = lim >> 2;   // dwords below this lie inside the packet
-                typedef __attribute__((address_space(1))) uint32_t g32;
-                while (j < je) {
-                    uint8_t* dst = base + 4 * j;
-                    if (!(j & 3) && j + 4 <= je && j + 4 <= jfull) {
-                        const v4u q = {slot[j], slot[j + 1], slot[j + 2], slot[j + 3]};
-                        *(__attribute__((address_space(1))) v4u*)dst = q;
-                        j += 4;
-                    } else if (!(j & 1) && j + 2 <= je && j + 2 <= jfull) {
-                        typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-                        const v2u q = {slot[j], slot[j + 1]};
-                        *(__attribute__((address_space(1))) v2u*)dst = q;
-                        j += 2;
-                    } else if (j + 1 <= jfull) {
-                        *(g32*)dst = slot[j];
-                        j += 1;
-                    } else {
-                        for (int q = 4 * j; q < lim; ++q) base[q] = w[q];
-                        j += 1;
-                    }
-                }
-            }
+            nat_store_range(base, slot, w, r0, len, a.lo, a.hi);
             if (STRICT) {
                 res[i] = (a.ip_dirty ? VPCSUM_F_IP : 0) | (a.l4_dirty ? VPCSUM_F_L4 : 0);
                 continue;
@@ -380,7 +413,58 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
     }
 }
 
+// Strict mode's status after the recompute kernel: that kernel reports a refused packet as
+// S_BAD_DESC only, so the TTL-expired ones (left untouched, their TTL byte still <= 1) get their
+// S_TTL_EXPIRED bit here, from the same test on the same bytes.
+template <int FMT>
+__global__ __launch_bounds__(256) void k_nat_ttl_status(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                       const uint4* __restrict__ desc, const void* __restrict__ rw,
+                                                       uint32_t n, uint8_t* __restrict__ status) {
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+        const NatRw r = nat_load_rw<FMT>(rw, p);
+        if (!(r.mask & VPCSUM_NAT_DEC_TTL)) continue;
+        const uint4 dv = desc[p];
+        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        const int len = dv.z & 0xffff, l4o = dv.z >> 16, ver = dv.w & 0xff;
+        if (nat_desc_ok(off, len, l4o, ver, arena_len, FMT) && nat_ttl_expired(arena + off, ver, r))
+            status[p] = (uint8_t)kNatExpired;
+    }
+}
+
+hipError_t launch_nat_ttl_status(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw,
+                                 int fmt, uint32_t n, uint8_t* status, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    uint32_t g = (n + 255) / 256;
+    const uint32_t cap = (uint32_t)num_cus(dev) * 8;
+    if (g > cap) g = cap;
+    if (fmt == 0)
+        hipLaunchKernelGGL(k_nat_ttl_status<0>, dim3(g), dim3(256), 0, stream, arena, arena_len, (const uint4*)desc, rw, n, status);
+    else
+        hipLaunchKernelGGL(k_nat_ttl_status<1>, dim3(g), dim3(256), 0, stream, arena, arena_len, (const uint4*)desc, rw, n, status);
+    return hipGetLastError();
+}
+
 constexpr int kNatWideLog2 = 1;   // packets per lane and iteration of k_natw: 2
+
+hipError_t launch_nat_probe(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw, int fmt,
+                            uint32_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    uint32_t g = (n + (256u << kNatWideLog2) - 1) / (256u << kNatWideLog2);   // as launch_nat
+    const uint32_t cap = (uint32_t)num_cus(dev) * 8;
+    if (g > cap) g = cap;
+    const uint4* d = (const uint4*)desc;
+    if (fmt == 0)
+        hipLaunchKernelGGL((k_natw<0, false, 1 << kNatWideLog2, true>), dim3(g), dim3(256), 0, stream, arena, arena_len,
+                           d, rw, n, (uint8_t*)nullptr, (uint8_t*)nullptr);
+    else
+        hipLaunchKernelGGL((k_natw<1, false, 1 << kNatWideLog2, true>), dim3(g), dim3(256), 0, stream, arena, arena_len,
+                           d, rw, n, (uint8_t*)nullptr, (uint8_t*)nullptr);
+    return hipGetLastError();
+}
 
 hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw, int fmt,
                       uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream) {

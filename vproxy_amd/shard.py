@@ -69,3 +69,14 @@ def all_ranks_ok(ok: bool) -> bool:
     t = torch.tensor([1 if ok else 0], dtype=torch.int32)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item())
+
+
+def gather_over_ranks(obj) -> list:
+    """Every rank's `obj` (a small JSON-able value) in rank order; [obj] without torch.distributed
+    (bench: per-rank kernel times and devices of a multi-GPU line)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out

@@ -18,6 +18,7 @@ from .build import LIB
 
 F_IP, F_L4, F_RAW, F_L4P = 0x01, 0x02, 0x04, 0x08
 S_IP_OK, S_L4_OK, S_UDP_NOCSUM, S_DONE, S_BAD_DESC = 0x01, 0x02, 0x04, 0x40, 0x80
+S_TTL_EXPIRED = 0x20
 MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
 NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL, NAT_SET_TTL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 NAT_RFC1624, NAT_STRICT_JAVA = 0x00, 0x01
@@ -38,7 +39,7 @@ EXPORTS = [
     "vpcsum_abi_version", "vpcsum_last_error", "vpcsum_device_count", "vpcsum_set_device",
     "vpcsum_compute_async", "vpcsum_nat4_async", "vpcsum_nat_async", "vpcsum_parse_ether_async",
     "vpcsum_parse_ether_tuples_async", "vpcsum_read_probe_async",
-    "vpcsum_pattern_probe_async",
+    "vpcsum_pattern_probe_async", "vpcsum_nat4_pattern_probe_async",
     "vpcsum_synth_async", "vpcsum_event_create", "vpcsum_event_destroy", "vpcsum_event_record",
     "vpcsum_event_elapsed_ms", "vpcsum_stream_sync", "vpcsum_ctx_create", "vpcsum_ctx_destroy",
     "vpcsum_ctx_register_arena", "vpcsum_ctx_unregister_arena", "vpcsum_ctx_submit", "vpcsum_ctx_wait",
@@ -46,7 +47,7 @@ EXPORTS = [
     "vpcsum_ctx_parse_frames",
     "vpcsum_ctx_nat_submit", "Java_io_vproxy_vpcsum_VPCsum_natSubmit",
     "vpcsum_group_create", "vpcsum_group_create_list", "vpcsum_group_destroy", "vpcsum_group_register_arena",
-    "vpcsum_group_submit", "vpcsum_group_wait",
+    "vpcsum_group_unregister_arena", "vpcsum_group_submit", "vpcsum_group_wait",
     "Java_io_vproxy_vpcsum_VPCsum_create", "Java_io_vproxy_vpcsum_VPCsum_registerArena",
     "Java_io_vproxy_vpcsum_VPCsum_submit", "Java_io_vproxy_vpcsum_VPCsum_waitFor",
     "Java_io_vproxy_vpcsum_VPCsum_close", "Java_io_vproxy_vpcsum_VPCsum_setService",
@@ -81,12 +82,14 @@ def _declare(L):
         "vpcsum_group_create_list": ([P, I, U64, U32, P], I),
         "vpcsum_group_destroy": ([P], I),
         "vpcsum_group_register_arena": ([P, P, U64], I),
+        "vpcsum_group_unregister_arena": ([P, P], I),
         "vpcsum_group_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
         "vpcsum_group_wait": ([P, U64], I),
         "vpcsum_parse_ether_async": ([P, U64, P, P, U32, U8, P, P, P], I),
         "vpcsum_parse_ether_tuples_async": ([P, U64, P, P, U32, U8, P, P, P, P], I),
         "vpcsum_read_probe_async": ([P, U64, P, U32, P], I),
         "vpcsum_pattern_probe_async": ([P, U64, P, U32, P, U32, P], I),
+        "vpcsum_nat4_pattern_probe_async": ([P, U64, P, P, U32, P], I),
         "vpcsum_synth_async": ([P, U64, U32, U32, U32, U32, U64, U64, P, P], I),
         "vpcsum_event_create": ([P], I),
         "vpcsum_event_destroy": ([P], I),
@@ -202,6 +205,12 @@ def pattern_probe(arena, desc, n: int, sink, grid: int = 0, stream=None):
     assert sink.numel() * sink.element_size() >= 4096, "sink needs 1024 words"
     _check(lib().vpcsum_pattern_probe_async(_ptr(arena), arena.numel(), _ptr(desc), n, _ptr(sink), grid,
                                             _stream(stream)), "vpcsum_pattern_probe_async")
+
+
+def nat4_pattern_probe(arena, desc, rw, n: int, stream=None):
+    """NAT's memory operations for `desc` / `rw` (16-B entries) with no rewrite (tooling)."""
+    _check(lib().vpcsum_nat4_pattern_probe_async(_ptr(arena), arena.numel(), _ptr(desc), _ptr(rw), n,
+                                                 _stream(stream)), "vpcsum_nat4_pattern_probe_async")
 
 
 def read_probe(buf, nbytes: int, sink, grid: int = 0, stream=None):
@@ -369,6 +378,10 @@ class Group:
     def register(self, arr: np.ndarray):
         _check(lib().vpcsum_group_register_arena(self.h, arr.ctypes.data, arr.nbytes), "vpcsum_group_register_arena")
         self._pinned[arr.ctypes.data] = arr
+
+    def unregister(self, arr: np.ndarray):
+        _check(lib().vpcsum_group_unregister_arena(self.h, arr.ctypes.data), "vpcsum_group_unregister_arena")
+        self._pinned.pop(arr.ctypes.data, None)
 
     def submit(self, arena: np.ndarray, desc: np.ndarray, out: np.ndarray, status: np.ndarray | None = None,
                mode: int = MODE_COMPUTE) -> int:

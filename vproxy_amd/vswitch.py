@@ -5,8 +5,13 @@ callers).  Same contract as java/io/vproxy/vpcsum/GpuCsumBatch.java:
   SwitchUtils.java:297-316): IP dirty -> F_IP (VP_CSUM_IP), upper layer dirty -> F_L4 (VP_CSUM_UP).
 * :class:`EgressBatch` -- defer dirty frames at Iface.sendPacket, compute every deferred sum at
   Iface.completeTx in one GPU launch, written into the frames (XDPIface.java:100-178, 227-243).
+* :func:`egress_descriptor` -- the descriptor GpuCsumBatch.defer builds from the parsed Java
+  packet of a frame vproxy holds (partially parsed: Ethernet padding and IPv4 options included in
+  the buffer, so the lengths come from the IP header fields, not from the buffer).
 * :func:`descriptors_for_frames` -- build descriptors for received Ethernet frames on the GPU
   (EthernetPacket/Ipv4Packet/Ipv6Packet.from rules) for ingress verify.
+* :func:`recalc_policy` -- the verify status -> DevInput csum-recalc decision (which frames get
+  their sums marked dirty, which are dropped), INTEGRATION.md §4.
 
 No checksum is computed on the CPU here: everything goes through libvpcsum.so.
 """
@@ -32,6 +37,56 @@ def checksum_flags_for(is_ipv4: bool, ip_dirty: bool, upper_proto: int, upper_di
     if upper_dirty and upper_proto in L4_WITH_CSUM and not (is_ipv4 and upper_proto == 58):
         f |= V.F_L4P if offload and upper_proto != 1 else V.F_L4
     return f
+
+
+# IPv6 next-header values Java parses as extension headers (Consts.IPv6_needs_next_header,
+# base/src/main/java/io/vproxy/base/util/Consts.java:31)
+IPV6_EXT_HEADERS = frozenset({0, 60, 43, 44, 51, 50, 135, 139, 140, 253, 254})
+
+
+def _u16(b, o: int) -> int:
+    return (int(b[o]) << 8) | int(b[o + 1])
+
+
+def egress_descriptor(frame, frame_off: int, flags: int):
+    """The descriptor GpuCsumBatch.defer fills for one frame, from what the Java packet objects
+    report (java/io/vproxy/vpcsum/GpuCsumBatch.java: defer):
+
+    * L3 at frame + 14, or + 18 with an 802.1Q tag (EthernetPacket.getVlan(), EthernetPacket.java:
+      32-37);
+    * IPv4: l3_len = Ipv4Packet.getTotalLength() and l4_off = getIhl() * 4 (:334, :361).  A frame
+      parsed with allowPartial (every XDP / tap frame: PacketBuffer.java:177 -> EthernetPacket.java:
+      52-56) keeps its Ethernet padding in pktBuf and leaves `options` empty (initPartial,
+      Ipv4Packet.java:29-63), so neither the buffer length nor getHeaderSize() may be used;
+      Java's own recompute covers raw.sub(ihl*4, totalLength - ihl*4) (:55);
+    * IPv6: l3_len = 40 + getPayloadLength() (:332), l4_off = getHeaderSize() (:427-435: 40 +
+      8 + hdrExtLen per extension header, which from() fills whenever the next header is one,
+      :33-35), l4_proto = getProtocol() (the last header's next header, :363-367).
+
+    `frame` holds the frame's bytes from its first byte: the header fields the Java object
+    exposes are read from it (no checksum is computed here).  Returns a DESC_DTYPE record, or None
+    for a frame that is not IP."""
+    b = frame
+    typ, hl = _u16(b, 12), 14
+    if typ == ETHER_TYPE_8021Q:
+        typ, hl = _u16(b, 16), 18
+    d = np.zeros(1, V.DESC_DTYPE)[0]
+    d["l3_off"] = frame_off + hl
+    d["flags"] = flags
+    if typ == ETHER_TYPE_IPv4:
+        d["l3_len"] = _u16(b, hl + 2)
+        d["l4_off"] = (int(b[hl]) & 0x0F) * 4
+        d["l3_ver"], d["l4_proto"] = 4, int(b[hl + 9])
+    elif typ == ETHER_TYPE_IPv6:
+        nh, off = int(b[hl + 6]), 40
+        if nh in IPV6_EXT_HEADERS:   # one extension header (a chain makes Java's parser loop)
+            nh, off = int(b[hl + 40]), 40 + 8 + int(b[hl + 41])
+        d["l3_len"] = 40 + _u16(b, hl + 4)
+        d["l4_off"] = off
+        d["l3_ver"], d["l4_proto"] = 6, nh
+    else:
+        return None
+    return d
 
 
 class EgressBatch:
@@ -74,8 +129,26 @@ class EgressBatch:
         self.n += 1
         return True
 
+    def defer_frame(self, frame_off: int, flags: int) -> bool:
+        """GpuCsumBatch.defer for a frame at `frame_off` of the arena: the descriptor comes from
+        the IP header fields (:func:`egress_descriptor`), never from the buffer length."""
+        self.stats["tx_pkts"] += 1
+        if flags == 0:
+            return False
+        d = egress_descriptor(self.arena[frame_off:frame_off + 64], frame_off, flags)
+        if d is None:
+            return False
+        if self.n == self.capacity:
+            self.complete_tx()
+        self.desc[self.n] = d
+        self.n += 1
+        return True
+
     def complete_tx(self) -> int:
-        """Iface.completeTx: flush every deferred checksum into the frames."""
+        """Iface.completeTx: flush every deferred checksum into the frames.  Returns the frames
+        the GPU wrote.  A descriptor the kernel rejects (S_BAD_DESC: nothing written) is handed
+        back with the small flushes (`handed_back`), as GpuCsumBatch.flush restores the chunk's
+        native VP_CSUM_* flags: the frame is never sent with a stale sum."""
         if self.n == 0:
             return 0
         n = self.n
@@ -86,16 +159,76 @@ class EgressBatch:
             return 0
         t = self.ctx.submit(self.arena, self.desc[:n], self.out[:n], self.status[:n], V.MODE_WRITE)
         self.ctx.wait(t)
-        bad = int(np.count_nonzero(self.status[:n] & V.S_BAD_DESC))
-        if bad:
-            raise V.VpcsumError(f"{bad} descriptors rejected by the checksum kernel")
-        self.stats["tx_csum_gpu"] += n
+        bad = (self.status[:n] & V.S_BAD_DESC) != 0
+        nbad = int(np.count_nonzero(bad))
+        if nbad:
+            self.handed_back.append(self.desc[:n][bad].copy())
+            self.stats["handed_back"] = self.stats.get("handed_back", 0) + nbad
+            self.stats["rejected"] = self.stats.get("rejected", 0) + nbad
+        self.stats["tx_csum_gpu"] += n - nbad
         self.stats["flushes"] += 1
         self.n = 0
-        return n
+        return n - nbad
 
     def close(self):
         self.ctx.close()
+
+
+CSUM_RECALC_NONE, CSUM_RECALC_ALL = "none", "all"     # CSumRecalcType.java:3-6
+
+
+class RecalcDecision:
+    """What DevInput does with each frame of a verified RX batch (see :func:`recalc_policy`)."""
+
+    def __init__(self, ip_dirty: np.ndarray, l4_dirty: np.ndarray, drop: np.ndarray, stats: dict):
+        self.ip_dirty, self.l4_dirty, self.drop, self.stats = ip_dirty, l4_dirty, drop, stats
+
+    def egress_flags(self) -> np.ndarray:
+        """F_IP / F_L4 per frame: the sums the egress batch must recompute for it (0: none)."""
+        return np.where(self.ip_dirty, V.F_IP, 0).astype(np.uint8) | np.where(self.l4_dirty, V.F_L4, 0).astype(np.uint8)
+
+
+def recalc_policy(status: np.ndarray, desc: np.ndarray, csum_recalc: str = CSUM_RECALC_ALL,
+                  drop_bad: bool = False) -> RecalcDecision:
+    """DevInput.handle's csum-recalc step (core/.../vswitch/node/DevInput.java:37-49) driven by the
+    GPU's ingress verify of the batch (status from MODE_VERIFY over the parse descriptors `desc`).
+
+    * ``none``: the stored sums are kept and nothing is marked dirty -- the reference's behaviour.
+    * ``all``: the reference clears the L4 checksum of every IP packet and the IPv4 header
+      checksum too (clearChecksum -> checksumSkipped, AbstractPacket.java:43-53), so egress
+      recomputes every sum.  A sum that verified is recomputed to the value it already holds, so
+      only the frames that fail need the dirty mark for the egress bytes to be identical: IPv4
+      header dirty iff S_IP_OK is missing, L4 dirty iff S_L4_OK is missing -- which includes a UDP
+      stored 0 (no checksum, S_UDP_NOCSUM), that Java's recompute replaces with a real sum.
+      A frame the parser refused (S_BAD_DESC) is PacketBytes to Java (EthernetPacket.java:60-64):
+      untouched.  Later rewrites (NAT, TTL) still dirty their sums through the setters.
+    * ``drop_bad`` (a new capability, off by default; meant for NIC-facing interfaces, not for
+      veth / tap peers whose host stack leaves CHECKSUM_PARTIAL sums): frames whose stored sums
+      fail are dropped instead of repaired.  A UDP stored 0 is legal (RFC 768) and kept.
+
+    The counts in ``stats`` are what an interface would add to its statistics
+    (IfaceStatistics: rx csum errors / repaired / dropped)."""
+    n = len(status)
+    parsed = (status & V.S_BAD_DESC) == 0
+    has_ip = parsed & ((desc["flags"] & V.F_IP) != 0)
+    has_l4 = parsed & ((desc["flags"] & V.F_L4) != 0)
+    ip_bad = has_ip & ((status & V.S_IP_OK) == 0)
+    l4_bad = has_l4 & ((status & V.S_L4_OK) == 0)
+    nocsum = has_l4 & ((status & V.S_UDP_NOCSUM) != 0)
+    bad = ip_bad | (l4_bad & ~nocsum)
+    none = np.zeros(n, bool)
+    if csum_recalc not in (CSUM_RECALC_NONE, CSUM_RECALC_ALL):
+        raise ValueError(f"csum-recalc {csum_recalc!r}: none | all (CSumRecalcType)")
+    drop = bad if drop_bad else none
+    if csum_recalc == CSUM_RECALC_ALL:
+        ip_dirty, l4_dirty = ip_bad & ~drop, l4_bad & ~drop
+    else:
+        ip_dirty, l4_dirty = none, none.copy()
+    stats = {"rx_frames": int(n), "rx_not_ip": int(np.count_nonzero(~parsed)),
+             "rx_csum_bad": int(np.count_nonzero(bad)), "rx_udp_nocsum": int(np.count_nonzero(nocsum)),
+             "rx_dropped": int(np.count_nonzero(drop)),
+             "rx_marked_dirty": int(np.count_nonzero(ip_dirty | l4_dirty))}
+    return RecalcDecision(ip_dirty, l4_dirty, drop, stats)
 
 
 def verify_frames(ctx: "V.Context", arena: np.ndarray, desc: np.ndarray):
