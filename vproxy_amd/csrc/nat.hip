@@ -414,15 +414,18 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
 }
 
 // Strict mode's status after the recompute kernel: that kernel reports a refused packet as
-// S_BAD_DESC only, so the TTL-expired ones (left untouched, their TTL byte still <= 1) get their
-// S_TTL_EXPIRED bit here, from the same test on the same bytes.
+// S_BAD_DESC only, so the TTL-expired ones get their S_TTL_EXPIRED bit here, from the same test on
+// the same bytes: a refused packet was left untouched.  Only refused packets are looked at (a TTL
+// of 2 decremented to 1 passed); the recompute kernel refuses exactly the packets the rewrite
+// refused, since its descriptor rules equal nat_desc_ok for the flags the rewrite hands it.
 template <int FMT>
 __global__ __launch_bounds__(256) void k_nat_ttl_status(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                        const uint4* __restrict__ desc, const void* __restrict__ rw,
                                                        uint32_t n, uint8_t* __restrict__ status) {
+    // status[p] is read before it is written, by this lane only
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const NatRw r = nat_load_rw<FMT>(rw, p);
-        if (!(r.mask & VPCSUM_NAT_DEC_TTL)) continue;
+        if (!(r.mask & VPCSUM_NAT_DEC_TTL) || status[p] != VPCSUM_S_BAD_DESC) continue;
         const uint4 dv = desc[p];
         const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
         const int len = dv.z & 0xffff, l4o = dv.z >> 16, ver = dv.w & 0xff;
