@@ -1294,3 +1294,47 @@ def test_group_register_unregister_cycle(V, orc):
     out, _ = g.run(arena, desc)
     assert np.array_equal(out, want)
     g.close()
+
+
+def test_full_size_c5_properties(V, orc):
+    """BASELINE config C5 at its full size: 10,000,000 x 1500 B IPv4 TCP/UDP in one 20.5-GB arena,
+    every packet's addresses and ports rewritten (RFC 1624, the bench's kernel and mask).
+    Size-independent properties over all 10M packets: every rewritten packet still verifies (IP and
+    L4 sums equal Java's full recompute of the new bytes), the rewritten fields hold the entries'
+    bytes, and the payload beyond the L4 checksum field is untouched.  A random sample of 2000
+    packets is regenerated on the host and rewritten by the oracle (Java setters + full
+    recompute): byte-equal."""
+    import torch
+    n, stride = 10_000_000, 2048
+    arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    V.synth(arena, n, stride, 0, O.SYNTH_C5, O.SEED, 0, d)
+    V.compute(arena, d, n, None, None, O.MODE_WRITE)
+    g = torch.Generator(device="cpu").manual_seed(55)
+    rw = torch.randint(0, 256, (n, 16), dtype=torch.uint8, generator=g)
+    rw[:, 12] = O.NAT_SRC | O.NAT_DST | O.NAT_SPORT | O.NAT_DPORT
+    rw[:, 13:] = 0
+    rw_d = rw.cuda()
+    rng = np.random.default_rng(56)
+    idx = np.sort(rng.choice(n, 2000, replace=False))
+    tail_before = torch.stack([arena[int(i) * stride + 48:int(i) * stride + 1500] for i in idx[:64]]).cpu()
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    V.nat4(arena, d, rw_d, n, st, O.NAT_RFC1624)
+    torch.cuda.synchronize()
+    assert bool((st == O.S_DONE).all())
+    vs = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    V.compute(arena, d, n, None, vs, O.MODE_VERIFY)
+    torch.cuda.synchronize()
+    assert bool(((vs & 3) == 3).all()), "a rewritten packet no longer verifies"
+    frames = arena.view(n, stride)
+    assert torch.equal(frames[:, 12:16].cpu(), rw[:, 0:4]) and torch.equal(frames[:, 16:20].cpu(), rw[:, 4:8])
+    assert torch.equal(frames[:, 20:24].cpu(), rw[:, 8:12])      # ports (TCP and UDP: at L4 + 0..3)
+    tail_after = torch.stack([arena[int(i) * stride + 48:int(i) * stride + 1500] for i in idx[:64]]).cpu()
+    assert torch.equal(tail_before, tail_after)
+    rw_np = rw.numpy().view(O.NAT4_DTYPE).reshape(-1)
+    for i in idx:
+        a1, d1 = orc.synth(1, stride, 0, O.SYNTH_C5, O.SEED, int(i))
+        orc.process(a1, d1, O.MODE_COMPUTE, write=True)
+        orc.nat4_java(a1, d1, rw_np[i:i + 1])
+        assert np.array_equal(frames[int(i)].cpu().numpy(), a1), int(i)
+    del arena, frames

@@ -21,6 +21,20 @@ modes = [("rfc1624", V.NAT_RFC1624), ("strict_java", V.NAT_STRICT_JAVA),
          ("rfc1624_bytewise", V.NAT_RFC1624 | 0x100), ("strict_java_bytewise", V.NAT_STRICT_JAVA | 0x100)]
 if "--sweep" in sys.argv:   # packets per lane of the wide kernel (nat_mode bits 12..14)
     modes += [(f"rfc1624_w{1 << k}", V.NAT_RFC1624 | ((k + 1) << 12)) for k in range(3)]
+if "--probe" in sys.argv:   # the pattern ceiling and the bench's form (no status), interleaved rounds
+    for rnd in range(3):
+        for name, fn in (("probe", lambda: V.nat4_pattern_probe(arena, d, rw, n)),
+                         ("rfc1624_nostatus", lambda: V.nat4(arena, d, rw, n, None, V.NAT_RFC1624))):
+            for _ in range(3):
+                fn()
+            e0, e1 = V.Event(), V.Event()
+            e0.record()
+            for _ in range(10):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_ms(e1) / 10
+            res.setdefault(name, []).append({"ms": round(ms, 4), "Mpps": round(n / ms / 1e3, 1)})
 for name, mode in modes:
     for _ in range(3):
         V.nat4(arena, d, rw, n, st, mode)

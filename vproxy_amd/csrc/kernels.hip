@@ -400,20 +400,14 @@ __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, ui
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     for (int rr = 0; rr * TEAM < nch; rr += U) {
         v4u v[U];
-        // Load u is dead for the whole wave when no team's packet has a chunk at (rr + u) * TEAM:
-        // the teams of a size-sorted iteration share a length class, so a short class skips its
-        // last loads and their consumption (C3's 576-B packets need 36 of the trip's 48 chunks).
-        bool need[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            need[u] = u == 0 || __builtin_amdgcn_ballot_w64((rr + u) * TEAM < nch) != 0;
             const int k = (rr + u) * TEAM + tl;
             const uint32_t bo = k < nch ? boff + ((uint32_t)k << 4) : kOutOfRange;
-            v[u] = need[u] ? __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0) : v4u{0u, 0u, 0u, 0u};
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, bo, 0, NT ? 2 : 0);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (!need[u]) continue;
             const int k = (rr + u) * TEAM + tl;
             if ((uint32_t)(k - klo) < kfast) {
                 acc_l4 = hsum(hsum(hsum(hsum(acc_l4, v[u].x), v[u].y), v[u].z), v[u].w);
