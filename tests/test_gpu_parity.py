@@ -262,8 +262,11 @@ def test_nat_wide_and_scalar_kernels(V, orc, pad, workload, packed):
     v4 = desc["l3_ver"] == 4
     assert np.all(want_st[~v4] == O.S_BAD_DESC)
     assert set(np.unique(want_st[v4])) <= {O.S_DONE, O.S_BAD_DESC | O.S_TTL_EXPIRED}
-    # default, byte-access kernel (bit 8), wide kernel with 1 / 2 / 4 packets per lane (bits 12..14)
-    for force_scalar in (0, 0x100, 0x1000, 0x2000, 0x3000):
+    # default, byte-access kernel (bit 8), wide kernel with 1 / 2 / 4 packets per lane (bits 12..14),
+    # 4- and 6-chunk windows (bits 16..17: packets that do not fit 4 take the byte path), grids of
+    # 3 and 16 workgroups per CU (bits 18..22)
+    for force_scalar in (0, 0x100, 0x1000, 0x2000, 0x3000, 0x10000, 0x20000, 0x23000, 0x20000 | (3 << 18),
+                         0x20000 | (16 << 18)):
         got, st = _gpu_nat(V, arena, desc, rw, V.NAT_RFC1624 | force_scalar)
         assert np.array_equal(st, want_st), force_scalar
         assert np.array_equal(got, want), force_scalar
@@ -1319,7 +1322,7 @@ def test_full_size_c5_properties(V, orc):
     idx = np.sort(rng.choice(n, 2000, replace=False))
     tail_before = torch.stack([arena[int(i) * stride + 48:int(i) * stride + 1500] for i in idx[:64]]).cpu()
     st = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    V.nat4(arena, d, rw_d, n, st, O.NAT_RFC1624)
+    V.nat4(arena, d, rw_d, n, st, V.NAT_RFC1624)
     torch.cuda.synchronize()
     assert bool((st == O.S_DONE).all())
     vs = torch.zeros(n, dtype=torch.uint8, device="cuda")

@@ -18,6 +18,7 @@
 // and vpcsum_nat_t (48 B, IPv4 and IPv6).  One lane per packet.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "vpcsum.h"
 #include "internal.h"
 #include "device_common.h"
@@ -245,11 +246,11 @@ __device__ __forceinline__ void store_bytes_packed(uint8_t* __restrict__ dst, ui
     const uint32_t b1 = (uint32_t)__shfl_down((int)v, 1, 64), b2 = (uint32_t)__shfl_down((int)v, 2, 64),
                    b3 = (uint32_t)__shfl_down((int)v, 3, 64);
     if ((threadIdx.x & 3) == 0 && p < n) {
+        const uint32_t packed = v | ((b1 & 0xff) << 8) | ((b2 & 0xff) << 16) | (b3 << 24);
         if (p + 4 <= n && !((uintptr_t)(dst + p) & 3)) {
-            *(__attribute__((address_space(1))) uint32_t*)(dst + p) = v | (b1 << 8) | (b2 << 16) | (b3 << 24);
-        } else {
-            const uint32_t b[4] = {v, b1, b2, b3};
-            for (uint32_t k = 0; k < 4 && p + k < n; ++k) dst[p + k] = (uint8_t)b[k];
+            *(__attribute__((address_space(1))) uint32_t*)(dst + p) = packed;
+        } else {   // shifts, not an indexed array: no scratch
+            for (uint32_t k = 0; k < 4 && p + k < n; ++k) dst[p + k] = (uint8_t)(packed >> (8 * k));
         }
     }
 }
@@ -309,27 +310,31 @@ __device__ __forceinline__ void nat_store_range(uint8_t* base, const uint32_t* s
         }
     }
 }
-constexpr int kNatSlotDw = 4 * kNatChunks + 1;  // LDS slot per lane: an odd dword stride (no bank conflicts)
 
 // PROBE: the same loads, LDS staging and stores with no rewrite -- the changed range is set to
 // what a rewrite of both addresses and ports produces ([10, L4 checksum end) for IPv4, [8, ..) for
 // IPv6) and the window is stored back unchanged.  It prices NAT's access pattern (the "pattern
 // ceiling" of BASELINE config C5): a rewrite cannot run faster than its own memory operations.
-template <int FMT, bool STRICT, int W, bool PROBE = false>
+// CH: window chunks (16 B each).  6 hold any header the wide path takes (IPv4 with options, IPv6
+// without extension headers, any alignment); 4 hold IPv4 + TCP / UDP without options at any L3
+// alignment (an umem frame puts L3 at chunk offset 14: 14 + 38 <= 64), and need 16 fewer VGPRs
+// at W = 2.  A packet whose header does not fit takes the byte-access path.
+template <int FMT, bool STRICT, int W, bool PROBE = false, int CH = kNatChunks>
 __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint64_t arena_len,
                                              const uint4* __restrict__ desc, const void* __restrict__ rw, uint32_t n,
                                              uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(1))) const v4u gv4u;
-    __shared__ uint32_t s_win[256 * kNatSlotDw];
-    uint32_t* slot = &s_win[threadIdx.x * kNatSlotDw];
+    constexpr int kSlotDw = 4 * CH + 1;   // LDS slot per lane: an odd dword stride (no bank conflicts)
+    __shared__ uint32_t s_win[256 * kSlotDw];
+    uint32_t* slot = &s_win[threadIdx.x * kSlotDw];
     uint8_t* w = (uint8_t*)slot;
     const uint32_t T = gridDim.x * blockDim.x;
     for (uint32_t p0 = blockIdx.x * blockDim.x + threadIdx.x; p0 < n; p0 += W * T) {
         uint4 dv[W];
         NatRw rr[W];
         int wend[W];
-        uint4 v[W][kNatChunks];
+        uint4 v[W][CH];
 #pragma unroll
         for (int i = 0; i < W; ++i) {
             const uint32_t p = p0 + i * T;
@@ -349,10 +354,10 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
             const int r0 = (int)(la & 15);
             int need = ver == 4 ? 20 : 40;
             if (nat_l4sum(ver, proto, len, l4o)) need = max(need, l4o + l4_field(proto) + 2);
-            wend[i] = ok && r0 + need <= 16 * kNatChunks ? r0 + need : 0;   // 0: the byte-access path
+            wend[i] = ok && r0 + need <= 16 * CH ? r0 + need : 0;   // 0: the byte-access path
             const uintptr_t base = la - (uintptr_t)r0;
 #pragma unroll
-            for (int k = 0; k < kNatChunks; ++k) {
+            for (int k = 0; k < CH; ++k) {
                 // only the chunks the packet needs: all lie in its 16-B blocks, which never cross
                 // a page, so none reads past the arena's last page
                 v4u x = {0u, 0u, 0u, 0u};
@@ -377,7 +382,7 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
             const int r0 = (int)(la & 15);
             uint8_t* base = (uint8_t*)(la - (uintptr_t)r0);
 #pragma unroll
-            for (int k = 0; k < kNatChunks; ++k) {
+            for (int k = 0; k < CH; ++k) {
                 if ((k << 4) < wend[i]) {
                     slot[4 * k] = v[i][k].x; slot[4 * k + 1] = v[i][k].y;
                     slot[4 * k + 2] = v[i][k].z; slot[4 * k + 3] = v[i][k].w;
@@ -451,45 +456,69 @@ hipError_t launch_nat_ttl_status(const uint8_t* arena, uint64_t arena_len, const
 
 constexpr int kNatWideLog2 = 1;   // packets per lane and iteration of k_natw: 2
 
+// Grid of the wide kernel: enough workgroups that one iteration of W packets per lane covers the
+// batch, capped at `wgs_per_cu` per CU (grid-stride beyond that).
+static uint32_t nat_grid(uint32_t n, int wl2, uint32_t wgs_per_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    uint32_t g = (n + (256u << wl2) - 1) / (256u << wl2);
+    const uint32_t cap = (uint32_t)num_cus(dev) * wgs_per_cu;
+    return g > cap ? cap : g;
+}
+
+// Internal tuning bits of nat_mode (not part of the stable ABI): bit 8 byte-access kernel; bits
+// 12..14 log2(packets per lane) + 1 of the wide kernel; bits 16..17 window chunks (1: 6, 2: 4);
+// bits 18..22 workgroups per CU (0: 8).
+static int nat_chunks_sel(uint32_t nat_mode, int fmt) {
+    const uint32_t c = (nat_mode >> 16) & 3u;
+    if (c == 1) return 6;
+    if (c == 2 && fmt == 0) return 4;
+    return kNatChunks;
+}
+static uint32_t nat_wgs_per_cu(uint32_t nat_mode) {
+    const uint32_t w = (nat_mode >> 18) & 31u;
+    return w ? w : 8u;
+}
+
 hipError_t launch_nat_probe(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw, int fmt,
                             uint32_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    uint32_t g = (n + (256u << kNatWideLog2) - 1) / (256u << kNatWideLog2);   // as launch_nat
-    const uint32_t cap = (uint32_t)num_cus(dev) * 8;
-    if (g > cap) g = cap;
+    // tooling: the tuning bits of nat_mode, to price the same shapes launch_nat can take
+    static const uint32_t tune = [] {
+        const char* e = getenv("VPCSUM_NAT_PROBE_TUNE");
+        return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+    }();
+    const uint32_t g = nat_grid(n, kNatWideLog2, nat_wgs_per_cu(tune));
     const uint4* d = (const uint4*)desc;
-    if (fmt == 0)
-        hipLaunchKernelGGL((k_natw<0, false, 1 << kNatWideLog2, true>), dim3(g), dim3(256), 0, stream, arena, arena_len,
-                           d, rw, n, (uint8_t*)nullptr, (uint8_t*)nullptr);
+    constexpr int W = 1 << kNatWideLog2;
+    if (fmt == 0 && nat_chunks_sel(tune, 0) == 4)
+        hipLaunchKernelGGL((k_natw<0, false, W, true, 4>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n,
+                           (uint8_t*)nullptr, (uint8_t*)nullptr);
+    else if (fmt == 0)
+        hipLaunchKernelGGL((k_natw<0, false, W, true>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n,
+                           (uint8_t*)nullptr, (uint8_t*)nullptr);
     else
-        hipLaunchKernelGGL((k_natw<1, false, 1 << kNatWideLog2, true>), dim3(g), dim3(256), 0, stream, arena, arena_len,
-                           d, rw, n, (uint8_t*)nullptr, (uint8_t*)nullptr);
+        hipLaunchKernelGGL((k_natw<1, false, W, true>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n,
+                           (uint8_t*)nullptr, (uint8_t*)nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw, int fmt,
                       uint32_t n, uint8_t* status, uint8_t* flags_out, uint32_t nat_mode, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
     const bool strict = (nat_mode & VPCSUM_NAT_STRICT_JAVA) != 0;
-    // nat_mode bits 12..14 (internal tuning): log2 packets per lane and iteration of the wide
-    // kernel + 1 (0 = default)
     const int wsel = (int)((nat_mode >> 12) & 7u);
     const int wl2 = wsel ? (wsel - 1 > 2 ? 2 : wsel - 1) : kNatWideLog2;
-    // one iteration of W packets per lane covers the batch when the chip holds the grid
-    uint32_t g = (n + (256u << wl2) - 1) / (256u << wl2);
-    const uint32_t cap = (uint32_t)num_cus(dev) * 8;
-    if (g > cap) g = cap;
-    // nat_mode bit 8 (internal tuning): force the byte-access kernel
+    const uint32_t g = nat_grid(n, wl2, nat_wgs_per_cu(nat_mode));
+    const int ch = nat_chunks_sel(nat_mode, fmt);
     const bool wide = !(nat_mode & 0x100u);
     const uint4* d = (const uint4*)desc;
     if (wide) {
-#define VPC_NAT(F, S, W) hipLaunchKernelGGL((k_natw<F, S, W>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out)
-#define VPC_NAT_W(F, S) do { if (wl2 == 0) VPC_NAT(F, S, 1); else if (wl2 == 1) VPC_NAT(F, S, 2); else VPC_NAT(F, S, 4); } while (0)
-        if (fmt == 0) {
+#define VPC_NAT(F, S, W, C) hipLaunchKernelGGL((k_natw<F, S, W, false, C>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out)
+#define VPC_NAT_W(F, S) do { if (wl2 == 0) VPC_NAT(F, S, 1, kNatChunks); else if (wl2 == 1) VPC_NAT(F, S, 2, kNatChunks); else VPC_NAT(F, S, 4, kNatChunks); } while (0)
+        if (fmt == 0 && !strict && ch == 4) {
+            if (wl2 == 2) VPC_NAT(0, false, 4, 4); else VPC_NAT(0, false, 2, 4);
+        } else if (fmt == 0) {
             if (strict) VPC_NAT_W(0, true); else VPC_NAT_W(0, false);
         } else {
             if (strict) VPC_NAT_W(1, true); else VPC_NAT_W(1, false);
@@ -503,5 +532,6 @@ hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d
     }
     return hipGetLastError();
 }
+
 
 }  // namespace vpcsum
