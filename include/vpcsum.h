@@ -276,6 +276,22 @@ int vpcsum_ctx_parse_frames(vpcsum_ctx_t* ctx, const uint8_t* h_arena, uint64_t 
                             const uint64_t* h_frame_off, const uint32_t* h_frame_len, uint32_t n,
                             vpcsum_desc_t* h_desc, uint8_t* h_status, vpcsum_tuple_t* h_tuples,
                             uint64_t* ticket);
+/* Egress flush straight from the frames (the alternative to building descriptors on the host): the
+ * frames at h_frame_off[i] (h_frame_len[i] bytes) of a registered arena, as the TX ring sends them
+ * (XDPIface.sendPacket: chunk.getAddr() + pkb.pktOff and pkb.pktBuf.length(), or the copy's
+ * pktaddr), each with the VPCSUM_F_* sums it needs (h_frame_flags[i]: F_IP / F_L4 / F_L4P, the
+ * mapping of SwitchUtils.checksumFlagsFor, SwitchUtils.java:297-316).  The GPU parses every frame
+ * with the vswitch's rules (as vpcsum_parse_ether_async: L3 after the Ethernet / 802.1Q header,
+ * lengths from totalLength / payloadLength, L4 after IHL / the extension header), so padding,
+ * options and extension headers are placed as Java's recompute places them, and writes the sums
+ * into the frames (MODE_WRITE), in one submission.  At vpcsum_ctx_wait h_status[i] is S_DONE, or
+ * S_BAD_DESC (nothing written) for a frame the parser refuses or whose flags it cannot honour (an
+ * IPv4 header sum on IPv6, an L4 sum its segment cannot hold, F_L4P for ICMPv4): hand such a frame
+ * back to the native path.  h_out (may be NULL): the sums, as vpcsum_ctx_submit. */
+int vpcsum_ctx_egress_frames(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena_len,
+                             const uint64_t* h_frame_off, const uint32_t* h_frame_len,
+                             const uint8_t* h_frame_flags, uint32_t n,
+                             uint32_t* h_out, uint8_t* h_status, uint64_t* ticket);
 /* NAT / TTL rewrites of host frames (SwitchUtils.applyNat for a batch): h_rw[i] rewrites the
  * packet of h_desc[i] in place in the caller's frames, with the checksums updated as Java's
  * recompute leaves them (nat_mode as vpcsum_nat_async).  Frames in a registered arena are
@@ -357,6 +373,12 @@ int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t c
 int Java_io_vproxy_vpcsum_VPCsum_parseFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                              void* frameOff, void* frameLen, int32_t n, void* desc, void* status,
                                              void* tuples);
+/* VPCsum.egressFrames(long ctx, MemorySegment arena, long arenaLen, MemorySegment frameOff,
+ *                     MemorySegment frameLen, MemorySegment frameFlags, int n, MemorySegment out,
+ *                     MemorySegment status) -> long ticket */
+int Java_io_vproxy_vpcsum_VPCsum_egressFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                              void* frameOff, void* frameLen, void* frameFlags, int32_t n, void* out,
+                                              void* status);
 /* VPCsum.natSubmit(long ctx, MemorySegment arena, long arenaLen, MemorySegment desc,
  *                  MemorySegment rw, int n, MemorySegment status, int natMode) -> long ticket */
 int Java_io_vproxy_vpcsum_VPCsum_natSubmit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,

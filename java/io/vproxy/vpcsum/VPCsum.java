@@ -201,6 +201,35 @@ public class VPCsum {
         return ENV.returnLong();
     }
 
+    private static final MethodHandle egressFramesMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
+        "Java_io_vproxy_vpcsum_VPCsum_egressFrames", long.class /* ctx */, MemorySegment.class /* arena */,
+        long.class /* arenaLen */, MemorySegment.class /* frameOff */, MemorySegment.class /* frameLen */,
+        MemorySegment.class /* frameFlags */, int.class /* n */, MemorySegment.class /* out */,
+        MemorySegment.class /* status */);
+
+    /** Egress flush straight from the frames: frameOff[i] (u64) / frameLen[i] (u32) as the TX ring
+     * sends them, frameFlags[i] (u8) the F_* sums each needs.  The GPU parses every frame with the
+     * vswitch's rules and writes its sums in place, in one submission; after {@link #waitFor}
+     * status[i] is S_DONE or S_BAD_DESC (refused, nothing written: hand the frame back).
+     * Returns a ticket. */
+    public long egressFrames(PNIEnv ENV, long ctx, MemorySegment arena, long arenaLen, MemorySegment frameOff,
+                             MemorySegment frameLen, MemorySegment frameFlags, int n, MemorySegment out,
+                             MemorySegment status) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) egressFramesMH.invokeExact(ENV.MEMORY, ctx, arena, arenaLen, frameOff, frameLen, frameFlags, n,
+                                                   out, status);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+        return ENV.returnLong();
+    }
+
     private static final MethodHandle natSubmitMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
         "Java_io_vproxy_vpcsum_VPCsum_natSubmit", long.class /* ctx */, MemorySegment.class /* arena */,
         long.class /* arenaLen */, MemorySegment.class /* desc */, MemorySegment.class /* rw */, int.class /* n */,

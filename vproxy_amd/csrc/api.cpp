@@ -874,6 +874,49 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
     return 0;
 }
 
+int vpcsum_ctx_egress_frames(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
+                             const uint32_t* h_frame_len, const uint8_t* h_frame_flags, uint32_t n, uint32_t* h_out,
+                             uint8_t* h_status, uint64_t* ticket) {
+    if (!c || !ticket) return fail("vpcsum_ctx_egress_frames: NULL context or ticket");
+    if (n > c->max_pkts) return fail("vpcsum_ctx_egress_frames: %u frames > capacity %u", n, c->max_pkts);
+    if (n && (!h_arena || !h_frame_off || !h_frame_len || !h_frame_flags))
+        return fail("vpcsum_ctx_egress_frames: NULL arena, frame table or flags");
+    std::lock_guard<std::mutex> lk(c->mu);
+    VPC_ON_DEVICE(c->device);
+    uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
+    if (n && !base) return fail("vpcsum_ctx_egress_frames: the arena must be registered (vpcsum_ctx_register_arena)");
+    const uint64_t t = c->next_ticket++;
+    Slot& s = c->slots[t & 1];
+    if (s.busy && slot_finish(c, s) != 0) return -1;
+    if (n) {
+        // the frames' own flags ride in the status staging: the parse reads them before the
+        // checksum kernel, later on the same stream, overwrites them with the statuses
+        memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
+        memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
+        memcpy(s.h_status, h_frame_flags, n);
+        VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, 0, s.d_desc, nullptr, nullptr, s.stream,
+                                     s.dh_status),
+                  "parse launch");
+        VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, s.dh_out, s.dh_status, nullptr, VPCSUM_MODE_COMPUTE, base,
+                              n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
+                  "checksum launch");
+    }
+    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+    s.zero_copy = true;
+    s.svc_seq = 0;
+    s.kind = 0;
+    s.busy = true;
+    s.ticket = t;
+    s.n = n;
+    s.mode = VPCSUM_MODE_WRITE;
+    s.user_arena = nullptr;   // written in place through the mapping
+    s.user_desc = nullptr;
+    s.user_out = h_out;
+    s.user_status = h_status;
+    *ticket = t;
+    return 0;
+}
+
 int vpcsum_ctx_parse_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
                             const uint32_t* h_frame_len, uint32_t n, vpcsum_desc_t* h_desc, uint8_t* h_status,
                             vpcsum_tuple_t* h_tuples, uint64_t* ticket) {
@@ -1304,6 +1347,22 @@ int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t c
     if (vpcsum_ctx_verify_frames((vpcsum_ctx_t*)(intptr_t)ctx, (const uint8_t*)arena, (uint64_t)arenaLen,
                                  (const uint64_t*)frameOff, (const uint32_t*)frameLen, (uint32_t)n, (uint32_t*)out,
                                  (uint8_t*)status, &t) != 0)
+        return pni_throw(env, "java.io.IOException");
+    env->return_ = (int64_t)t;
+    return 0;
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_egressFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                              void* frameOff, void* frameLen, void* frameFlags, int32_t n, void* out,
+                                              void* status) {
+    if (n < 0 || arenaLen < 0) {
+        fail("egressFrames: negative size");
+        return pni_throw(env, "java.lang.IllegalArgumentException");
+    }
+    uint64_t t = 0;
+    if (vpcsum_ctx_egress_frames((vpcsum_ctx_t*)(intptr_t)ctx, (uint8_t*)arena, (uint64_t)arenaLen,
+                                 (const uint64_t*)frameOff, (const uint32_t*)frameLen, (const uint8_t*)frameFlags,
+                                 (uint32_t)n, (uint32_t*)out, (uint8_t*)status, &t) != 0)
         return pni_throw(env, "java.io.IOException");
     env->return_ = (int64_t)t;
     return 0;

@@ -54,7 +54,8 @@ hipError_t launch_nat_ttl_status(const uint8_t* arena, uint64_t arena_len, const
 
 hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const uint64_t* frame_off,
                               const uint32_t* frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* desc,
-                              uint8_t* status, vpcsum_tuple_t* tuples, hipStream_t stream);
+                              uint8_t* status, vpcsum_tuple_t* tuples, hipStream_t stream,
+                              const uint8_t* frame_flags = nullptr);
 
 hipError_t launch_read_probe(const uint8_t* buf, uint64_t bytes, uint32_t* sink, uint32_t grid, hipStream_t stream);
 hipError_t launch_pattern_probe(const uint8_t* arena, uint64_t arena_len, const void* desc, uint32_t n, uint32_t* sink,

@@ -1410,6 +1410,7 @@ __device__ bool pe_ipv6_from(const uint8_t* b, uint32_t avail, uint32_t& total, 
 __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                     const uint64_t* __restrict__ foff,
                                                     const uint32_t* __restrict__ flen, uint32_t n, uint8_t want,
+                                                    const uint8_t* __restrict__ fwant,
                                                     vpcsum_desc_t* __restrict__ desc, uint8_t* __restrict__ status,
                                                     vpcsum_tuple_t* __restrict__ tuples) {
     // 64 tuples of a wave are staged here and written as 10 coalesced 256-B stores
@@ -1469,12 +1470,24 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
             }
         }
         if (st == 0) {
+            // fwant (egress): the frame's own flags, all of which must be honoured -- a frame that
+            // cannot take one (an IPv4 header sum on IPv6, an L4 sum its segment does not hold, a
+            // pseudo-header sum for ICMPv4) is refused, so nothing is written and the caller hands
+            // it back.  want (ingress): the sums the frame allows, of those asked.
+            const uint8_t w = fwant ? fwant[p] : want;
             uint8_t fl = 0;
-            if ((want & VPCSUM_F_IP) && d.l3_ver == 4) fl |= VPCSUM_F_IP;
+            const bool ip_ok = d.l3_ver == 4;
             const int fld = l4_field(d.l4_proto);
-            if ((want & VPCSUM_F_L4) && fld >= 0 && !(d.l3_ver == 4 && d.l4_proto == 58) &&
-                d.l3_len - d.l4_off >= fld + 2)
-                fl |= VPCSUM_F_L4;
+            const bool l4_ok = fld >= 0 && !(d.l3_ver == 4 && d.l4_proto == 58) && d.l3_len - d.l4_off >= fld + 2;
+            if ((w & VPCSUM_F_IP) && ip_ok) fl |= VPCSUM_F_IP;
+            if ((w & VPCSUM_F_L4) && l4_ok) fl |= VPCSUM_F_L4;
+            else if ((w & VPCSUM_F_L4P) && l4_ok && d.l4_proto != 1) fl |= VPCSUM_F_L4P;
+            if (fwant && (fl != (w & (VPCSUM_F_IP | VPCSUM_F_L4 | VPCSUM_F_L4P)) ||
+                          (w & ~(VPCSUM_F_IP | VPCSUM_F_L4 | VPCSUM_F_L4P)) || (fl & VPCSUM_F_L4 && fl & VPCSUM_F_L4P))) {
+                st = VPCSUM_S_BAD_DESC;
+                d.l3_off = 0; d.l3_len = 0; d.l4_off = 0; d.l3_ver = 0; d.l4_proto = 0;
+                fl = 0;
+            }
             d.flags = fl;
         }
         if (act) {
@@ -1527,12 +1540,13 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
 
 hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const uint64_t* frame_off,
                               const uint32_t* frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* desc,
-                              uint8_t* status, vpcsum_tuple_t* tuples, hipStream_t stream) {
+                              uint8_t* status, vpcsum_tuple_t* tuples, hipStream_t stream,
+                              const uint8_t* frame_flags) {
     if (n == 0) return hipSuccess;
     uint32_t g = (n + 255) / 256;
     if (g > 65535u * 8) g = 65535u * 8;
     hipLaunchKernelGGL(k_parse_ether, dim3(g), dim3(256), 0, stream, arena, arena_len, frame_off, frame_len, n,
-                       flags, desc, status, tuples);
+                       flags, frame_flags, desc, status, tuples);
     return hipGetLastError();
 }
 

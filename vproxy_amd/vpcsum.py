@@ -44,7 +44,7 @@ EXPORTS = [
     "vpcsum_event_elapsed_ms", "vpcsum_stream_sync", "vpcsum_ctx_create", "vpcsum_ctx_destroy",
     "vpcsum_ctx_register_arena", "vpcsum_ctx_unregister_arena", "vpcsum_ctx_submit", "vpcsum_ctx_wait",
     "vpcsum_ctx_pipeline", "vpcsum_ctx_set_service", "vpcsum_ctx_stats", "vpcsum_ctx_verify_frames",
-    "vpcsum_ctx_parse_frames",
+    "vpcsum_ctx_parse_frames", "vpcsum_ctx_egress_frames", "Java_io_vproxy_vpcsum_VPCsum_egressFrames",
     "vpcsum_ctx_nat_submit", "Java_io_vproxy_vpcsum_VPCsum_natSubmit",
     "vpcsum_group_create", "vpcsum_group_create_list", "vpcsum_group_destroy", "vpcsum_group_register_arena",
     "vpcsum_group_unregister_arena", "vpcsum_group_submit", "vpcsum_group_wait",
@@ -104,6 +104,7 @@ def _declare(L):
         "vpcsum_ctx_stats": ([P, P, P], I),
         "vpcsum_ctx_verify_frames": ([P, P, U64, P, P, U32, P, P, P], I),
         "vpcsum_ctx_parse_frames": ([P, P, U64, P, P, U32, P, P, P, P], I),
+        "vpcsum_ctx_egress_frames": ([P, P, U64, P, P, P, U32, P, P, P], I),
         "vpcsum_ctx_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
         "vpcsum_ctx_wait": ([P, U64], I),
         "vpcsum_ctx_pipeline": ([P, P, U32, U32, P, U32, P, U32, U32], I),
@@ -311,6 +312,24 @@ class Context:
                                              ctypes.byref(t)), "vpcsum_ctx_parse_frames")
         self.wait(t.value)
         return desc, status, tuples
+
+    def egress_frames(self, arena: np.ndarray, frame_off: np.ndarray, frame_len: np.ndarray,
+                      frame_flags: np.ndarray):
+        """Egress flush of frames in a registered arena, each with its own F_* flags: parsed on
+        the GPU and written in place in one submission (vpcsum_ctx_egress_frames).  Returns
+        (out, status) per frame; S_BAD_DESC = refused, nothing written."""
+        n = len(frame_off)
+        fo = np.ascontiguousarray(frame_off, dtype=np.uint64)
+        fl = np.ascontiguousarray(frame_len, dtype=np.uint32)
+        ff = np.ascontiguousarray(frame_flags, dtype=np.uint8)
+        out = np.zeros(n, np.uint32)
+        status = np.zeros(n, np.uint8)
+        t = ctypes.c_uint64()
+        _check(lib().vpcsum_ctx_egress_frames(self.h, arena.ctypes.data, arena.nbytes, fo.ctypes.data, fl.ctypes.data,
+                                              ff.ctypes.data, n, out.ctypes.data, status.ctypes.data,
+                                              ctypes.byref(t)), "vpcsum_ctx_egress_frames")
+        self.wait(t.value)
+        return out, status
 
     def nat_submit(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray, status: np.ndarray | None = None,
                    nat_mode: int = NAT_RFC1624) -> int:
