@@ -49,6 +49,13 @@ public final class GpuCsumBatch implements AutoCloseable {
     private final ChunkInfo[] chunks;
     private final int[] nativeFlagsOf;
     private int n = 0;
+    // deferFrame: raw frames whose descriptors the GPU builds itself (VPCsum.egressFrames)
+    private final MemorySegment frameOff;
+    private final MemorySegment frameLen;
+    private final MemorySegment frameFlags;
+    private final ChunkInfo[] frameChunks;
+    private final int[] frameNativeFlags;
+    private int nFrames = 0;
 
     /** Flushes of fewer frames go back to the native VP_CSUM_* path (the GPU breaks even at about
      * 5 frames per flush with the service grid, DESIGN.md §8). */
@@ -67,10 +74,47 @@ public final class GpuCsumBatch implements AutoCloseable {
         this.status = arena.allocate(capacity, 16);
         this.chunks = new ChunkInfo[capacity];
         this.nativeFlagsOf = new int[capacity];
+        this.frameOff = arena.allocate(8L * capacity, 16);
+        this.frameLen = arena.allocate(4L * capacity, 16);
+        this.frameFlags = arena.allocate(capacity, 16);
+        this.frameChunks = new ChunkInfo[capacity];
+        this.frameNativeFlags = new int[capacity];
+    }
+
+    /**
+     * The alternative to {@link #defer}: nothing is read from the Java packet objects.  The frame
+     * is handed over as XDPIface.sendPacket already has it -- its umem offset {@code pktaddr}
+     * (chunk.getAddr() + pkb.pktOff, or the copy's address) and {@code pktlen}
+     * (pkb.pktBuf.length(), Ethernet padding included) -- with the sums checksumFlagsFor asked for,
+     * and the GPU parses it with the vswitch's rules (L3 after the Ethernet / 802.1Q header,
+     * lengths from totalLength / payloadLength, L4 after IHL or the extension header) before it
+     * writes the sums (vpcsum_ctx_egress_frames).  Returns the flags the chunk keeps, as
+     * {@link #defer}; a frame the GPU refuses gets its native flags back at {@link #flush}.
+     */
+    public int deferFrame(ChunkInfo chunk, long pktaddr, int pktlen, int nativeFlags) {
+        int flags = 0;
+        int keep = nativeFlags & XDPConsts.VP_CSUM_XDP_OFFLOAD;
+        if ((nativeFlags & XDPConsts.VP_CSUM_IP) != 0) flags |= VPCsum.F_IP;
+        if ((nativeFlags & XDPConsts.VP_CSUM_UP) != 0) flags |= VPCsum.F_L4;
+        // the GPU refuses F_L4P for an ICMPv4 message (no pseudo header) and hands it back whole
+        if ((nativeFlags & XDPConsts.VP_CSUM_UP_PSEUDO) != 0) flags |= VPCsum.F_L4P;
+        if (flags == 0) {
+            return nativeFlags;
+        }
+        if (nFrames == capacity) {
+            throw new IllegalStateException("batch full: flush first");
+        }
+        frameOff.setAtIndex(ValueLayout.JAVA_LONG, nFrames, pktaddr);
+        frameLen.setAtIndex(ValueLayout.JAVA_INT, nFrames, pktlen);
+        frameFlags.set(ValueLayout.JAVA_BYTE, nFrames, (byte) flags);
+        frameChunks[nFrames] = chunk;
+        frameNativeFlags[nFrames] = nativeFlags;
+        ++nFrames;
+        return keep;
     }
 
     public boolean isFull() {
-        return n == capacity;
+        return n == capacity || nFrames == capacity;
     }
 
     /**
@@ -150,6 +194,36 @@ public final class GpuCsumBatch implements AutoCloseable {
      * computes its sums at xsk.writePackets instead of the frame leaving with a stale checksum.
      */
     public int flush() throws IOException {
+        return flushDescriptors() + flushFrames();
+    }
+
+    private int flushFrames() throws IOException {
+        if (nFrames == 0) {
+            return 0;
+        }
+        int done = nFrames;
+        if (nFrames < SMALL_FLUSH) {
+            for (int i = 0; i < nFrames; ++i) {
+                frameChunks[i].setCsumFlags(frameNativeFlags[i]);
+                frameChunks[i] = null;
+            }
+            nFrames = 0;
+            return 0;
+        }
+        long t = VPCsum.get().egressFrames(env, ctx, umem, umemLen, frameOff, frameLen, frameFlags, nFrames, out, status);
+        VPCsum.get().waitFor(env, ctx, t);
+        for (int i = 0; i < nFrames; ++i) {
+            if ((status.get(ValueLayout.JAVA_BYTE, i) & VPCsum.S_BAD_DESC) != 0) {
+                frameChunks[i].setCsumFlags(frameNativeFlags[i]);
+                --done;
+            }
+            frameChunks[i] = null;
+        }
+        nFrames = 0;
+        return done;
+    }
+
+    private int flushDescriptors() throws IOException {
         if (n == 0) {
             return 0;
         }

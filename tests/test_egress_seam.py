@@ -110,3 +110,54 @@ def test_egress_rejected_descriptor_is_handed_back(V, orc):
     assert np.array_equal(arena[o:o + 128], before7)
     assert np.array_equal(arena, want)
     batch.close()
+
+
+@pytest.mark.gpu
+def test_egress_frames_parsed_on_gpu(V, orc):
+    """vpcsum_ctx_egress_frames (FrameEgressBatch / VPCsum.egressFrames): only the frame offsets,
+    the frame lengths as the TX ring sends them (padding and trailers included) and per-frame flags
+    go to the GPU, which places L3 / L4 itself.  The umem equals the oracle's full recompute of
+    the same frames, byte for byte."""
+    from vproxy_amd import vswitch as S
+    fs, arena, offs, flags = _batch()
+    want = arena.copy()
+    orc.process(want, E.oracle_descriptors(fs, offs, flags), O.MODE_COMPUTE, write=True)
+    b = S.FrameEgressBatch(arena, capacity=len(fs))
+    for f, o, fl in zip(fs, offs, flags):
+        assert b.defer(o, len(f["frame"]), fl)
+    assert b.complete_tx() == len(fs) and not b.handed_back
+    assert np.array_equal(arena, want)
+    b.close()
+
+
+@pytest.mark.gpu
+def test_egress_frames_refusals(V, orc):
+    """Frames the GPU cannot honour are refused whole -- S_BAD_DESC, nothing written -- and handed
+    back: an IPv4 header sum asked of IPv6, a pseudo-header sum asked of ICMPv4 (it has none), an
+    ARP frame, a frame cut inside its IPv4 header, F_L4 and F_L4P together, F_RAW.  The others of
+    the same flush are written."""
+    from vproxy_amd import vswitch as S
+    fs, arena, offs, flags = _batch()
+    v6 = next(i for i, f in enumerate(fs) if f["ver"] == 6 and f["proto"] == 6)
+    icmp4 = next(i for i, f in enumerate(fs) if f["ver"] == 4 and f["proto"] == 1)
+    v4a, v4b, v4c, v4d = [i for i, f in enumerate(fs) if f["ver"] == 4 and f["proto"] == 6][:4]
+    lens = [len(f["frame"]) for f in fs]
+    bad = {v6: O.F_IP | O.F_L4, icmp4: O.F_L4P, v4a: O.F_L4 | O.F_L4P, v4b: O.F_RAW}
+    for i, fl in bad.items():
+        flags[i] = fl
+    hl = 18 if fs[v4c]["vlan"] else 14
+    arena[offs[v4c] + hl - 2:offs[v4c] + hl] = [0x08, 0x06]      # ARP
+    bad[v4c] = flags[v4c]
+    lens[v4d] = (18 if fs[v4d]["vlan"] else 14) + 12               # cut inside the IPv4 header
+    bad[v4d] = flags[v4d]
+    good = [i for i in range(len(fs)) if i not in bad]
+    want = arena.copy()
+    orc.process(want, E.oracle_descriptors([fs[i] for i in good], [offs[i] for i in good],
+                                           [flags[i] for i in good]), O.MODE_COMPUTE, write=True)
+    b = S.FrameEgressBatch(arena, capacity=len(fs))
+    for o, L, fl in zip(offs, lens, flags):
+        b.defer(o, L, fl)
+    assert b.complete_tx() == len(good)
+    assert sorted(x[0] for x in b.handed_back) == sorted(offs[i] for i in bad)
+    assert np.array_equal(arena, want)
+    b.close()

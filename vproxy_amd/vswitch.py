@@ -174,6 +174,48 @@ class EgressBatch:
         self.ctx.close()
 
 
+class FrameEgressBatch:
+    """The egress seam without host-side descriptors (vpcsum_ctx_egress_frames, the Java form is
+    VPCsum.egressFrames): ``defer`` records only what XDPIface.sendPacket already has -- the frame's
+    umem offset and length (chunk.getAddr() + pkb.pktOff, pkb.pktBuf.length(): padding included)
+    and its F_* flags -- and ``complete_tx`` has the GPU parse the frames with the vswitch's rules and
+    write their sums in place, in one submission.  A frame the GPU refuses (not parsable as IP, or
+    flags it cannot honour) is handed back untouched (``handed_back``)."""
+
+    def __init__(self, arena: np.ndarray, capacity: int = 4096, device: int = 0):
+        self.arena = arena
+        self.capacity = capacity
+        self.ctx = V.Context(device, max_arena=max(arena.nbytes, 1 << 16), max_pkts=capacity)
+        self.ctx.register(arena)
+        self.off = np.zeros(capacity, np.uint64)
+        self.len = np.zeros(capacity, np.uint32)
+        self.flags = np.zeros(capacity, np.uint8)
+        self.n = 0
+        self.handed_back: list[tuple[int, int, int]] = []
+
+    def defer(self, frame_off: int, frame_len: int, flags: int) -> bool:
+        if flags == 0:
+            return False
+        if self.n == self.capacity:
+            self.complete_tx()
+        self.off[self.n], self.len[self.n], self.flags[self.n] = frame_off, frame_len, flags
+        self.n += 1
+        return True
+
+    def complete_tx(self) -> int:
+        n = self.n
+        if n == 0:
+            return 0
+        _, st = self.ctx.egress_frames(self.arena, self.off[:n], self.len[:n], self.flags[:n])
+        bad = np.nonzero(st & V.S_BAD_DESC)[0]
+        self.handed_back += [(int(self.off[i]), int(self.len[i]), int(self.flags[i])) for i in bad]
+        self.n = 0
+        return n - len(bad)
+
+    def close(self):
+        self.ctx.close()
+
+
 CSUM_RECALC_NONE, CSUM_RECALC_ALL = "none", "all"     # CSumRecalcType.java:3-6
 
 
