@@ -161,3 +161,32 @@ def test_egress_frames_refusals(V, orc):
     assert sorted(x[0] for x in b.handed_back) == sorted(offs[i] for i in bad)
     assert np.array_equal(arena, want)
     b.close()
+
+
+def test_egress_descriptor_random_frames():
+    """2000 random frames as vproxy could hold them (IPv4 with IHL 5-15, IPv6 with 0 or 1 extension
+    header, TCP / UDP / ICMP / ICMPv6 / other, 802.1Q or not, 0-40 B of padding or trailer): for
+    every frame the reference's parser accepts, the mirror's descriptor equals the oracle's."""
+    from vproxy_amd import vswitch as S
+    rng = np.random.default_rng(2024)
+    n_ok = 0
+    for i in range(2000):
+        vlan = bool(rng.integers(0, 2))
+        ver = 4 if rng.random() < 0.6 else 6
+        proto = int(rng.choice([6, 17, 1, 58, 47]))
+        l4len = int(rng.integers(20, 300))
+        if ver == 4:
+            l3 = E._ipv4(rng, proto, l4len, int(rng.integers(5, 16)))
+        else:
+            l3 = E._ipv6(rng, proto, l4len, None if rng.random() < 0.5 else int(rng.integers(0, 64)))
+        f = E._ether(rng, l3, ver, vlan, trailer=int(rng.integers(0, 41)))
+        info, _ = O.parse_ether(f)
+        if info is None:
+            continue
+        n_ok += 1
+        fl = O.desc_flags_for(info)
+        d = S.egress_descriptor(np.frombuffer(f[:64], np.uint8), 1000, fl)
+        want = (1000 + info.l3_off, info.l3_len, info.l4_off, info.ver, info.proto, fl)
+        got = (int(d["l3_off"]), int(d["l3_len"]), int(d["l4_off"]), int(d["l3_ver"]), int(d["l4_proto"]), int(d["flags"]))
+        assert got == want, (i, got, want)
+    assert n_ok > 1500
