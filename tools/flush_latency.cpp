@@ -44,8 +44,23 @@ int main(int argc, char** argv) {
         desc[i].flags = VPCSUM_F_IP | VPCSUM_F_L4;
     }
     std::vector<uint32_t> out(nmax);
+    // the same frames behind a 14-B Ethernet header, for the egress path that parses raw frames on
+    // the GPU (vpcsum_ctx_egress_frames: offsets, lengths and per-frame flags only)
+    std::vector<uint8_t> eth((size_t)nmax * stride + 4096, 0);
+    std::vector<uint64_t> foff(nmax);
+    std::vector<uint32_t> flen(nmax);
+    std::vector<uint8_t> fflags(nmax, VPCSUM_F_IP | VPCSUM_F_L4);
+    std::vector<uint8_t> fst(nmax);
+    for (uint32_t i = 0; i < nmax; ++i) {
+        uint8_t* f = eth.data() + (size_t)i * stride;
+        f[12] = 0x08;
+        frame(f + 14, i);
+        foff[i] = (uint64_t)i * stride;
+        flen[i] = 1514;
+    }
     vpcsum_ctx_t* ctx = nullptr;
-    if (vpcsum_ctx_create(0, arena.size(), nmax, &ctx) || vpcsum_ctx_register_arena(ctx, arena.data(), arena.size())) {
+    if (vpcsum_ctx_create(0, eth.size(), nmax, &ctx) || vpcsum_ctx_register_arena(ctx, arena.data(), arena.size()) ||
+        vpcsum_ctx_register_arena(ctx, eth.data(), eth.size())) {
         fprintf(stderr, "setup: %s\n", vpcsum_last_error());
         return 1;
     }
@@ -53,29 +68,34 @@ int main(int argc, char** argv) {
     // only (no inline descriptors in the command line); 3 = frame loads clamped to the last chunk
     // (re-loads) instead of predicated; 4 = release semantics on the completion count and `done`.  The configurations run interleaved in kRounds rounds of
     // iters / kRounds flushes per size, so that drift on the box hits all of them alike.
-    static const char* names[5] = {"launch", "service", "service_no_inline", "service_clamped_loads",
-                                  "service_release_done"};
+    // 5 = raw frames parsed on the GPU, two launches per flush (vpcsum_ctx_egress_frames).
+    constexpr int kCfg = 6;
+    static const char* names[kCfg] = {"launch", "service", "service_no_inline", "service_clamped_loads",
+                                      "service_release_done", "egress_frames"};
     static const uint32_t sizes[7] = {1u, 3u, 4u, 32u, 128u, 1024u, 8192u};
     constexpr int kRounds = 5;
-    std::vector<double> us[5][7];
+    std::vector<double> us[kCfg][7];
     for (int r = 0; r < kRounds; ++r) {
-        for (int svc = 0; svc < 5; ++svc) {
+        for (int svc = 0; svc < kCfg; ++svc) {
             setenv("VPCSUM_SVC_INLINE", svc == 2 ? "0" : "1", 1);
             setenv("VPCSUM_SVC_CLAMP", svc == 3 ? "1" : "0", 1);
             setenv("VPCSUM_SVC_RELEASE_DONE", svc == 4 ? "1" : "0", 1);
-            if (vpcsum_ctx_set_service(ctx, svc ? 200000 : 0)) {
+            if (vpcsum_ctx_set_service(ctx, (svc && svc < 5) ? 200000 : 0)) {
                 fprintf(stderr, "service: %s\n", vpcsum_last_error());
                 return 1;
             }
             for (int si = 0; si < 7; ++si) {
                 const uint32_t b = sizes[si];
-                if (svc >= 2 && b > 128) break;
+                if (svc >= 2 && svc < 5 && b > 128) break;
                 for (int it = 0; it < iters / kRounds + 20; ++it) {
                     uint64_t t = 0;
                     const auto t0 = std::chrono::steady_clock::now();
-                    if (vpcsum_ctx_submit(ctx, arena.data(), arena.size(), desc.data(), b, out.data(), nullptr,
-                                          VPCSUM_MODE_WRITE, &t) ||
-                        vpcsum_ctx_wait(ctx, t)) {
+                    const int rc = svc == 5
+                        ? vpcsum_ctx_egress_frames(ctx, eth.data(), eth.size(), foff.data(), flen.data(), fflags.data(),
+                                                   b, out.data(), fst.data(), &t)
+                        : vpcsum_ctx_submit(ctx, arena.data(), arena.size(), desc.data(), b, out.data(), nullptr,
+                                            VPCSUM_MODE_WRITE, &t);
+                    if (rc || vpcsum_ctx_wait(ctx, t)) {
                         fprintf(stderr, "flush: %s\n", vpcsum_last_error());
                         return 1;
                     }
@@ -87,7 +107,7 @@ int main(int argc, char** argv) {
     }
     printf("{");
     const char* sep = "";
-    for (int svc = 0; svc < 5; ++svc) {
+    for (int svc = 0; svc < kCfg; ++svc) {
         printf("%s\"%s\": {", sep, names[svc]);
         sep = ", ";
         const char* sep2 = "";
