@@ -329,6 +329,27 @@ int vpcsum_group_unregister_arena(vpcsum_group_t* g, void* h_arena);
 int vpcsum_group_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
                         uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket);
 int vpcsum_group_wait(vpcsum_group_t* g, uint64_t ticket);
+/* as vpcsum_ctx_nat_submit, cut over the group's devices like vpcsum_group_submit; h_rw[i]
+ * rewrites the packet of h_desc[i]; the ticket is joined by vpcsum_group_wait */
+int vpcsum_group_nat_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                            const vpcsum_nat_t* h_rw, uint32_t n, uint8_t* h_status, uint32_t nat_mode,
+                            uint64_t* ticket);
+
+/* ------------------------------------------------------------------------ */
+/* SURVEY.md §8(b)'s entry points: the same over ONE process-wide group.     */
+/* vpcsum_init(dev_mask) creates it (error if one exists), vpcsum_shutdown   */
+/* destroys it; the others fail with "vpcsum_init first" before it.  The     */
+/* handle of a submit is waited on with vpcsum_batch_wait (checksum and NAT  */
+/* batches alike).                                                           */
+/* ------------------------------------------------------------------------ */
+int vpcsum_init(uint64_t dev_mask, uint64_t max_arena_bytes, uint32_t max_pkts);
+int vpcsum_shutdown(void);
+int vpcsum_register_arena(void* h_arena, uint64_t len);
+int vpcsum_batch_submit(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, uint32_t n,
+                        uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* handle);
+int vpcsum_nat_submit(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, const vpcsum_nat_t* h_rw,
+                      uint32_t n, uint8_t* h_status, uint32_t nat_mode, uint64_t* handle);
+int vpcsum_batch_wait(uint64_t handle);
 
 /* ------------------------------------------------------------------------ */
 /* PNI entry points (bound by io.vproxy.vpcsum.VPCsum)   */

@@ -137,3 +137,47 @@ def test_device_group_failed_submit_joins_submitted_ranges(orc):
     o2, _ = g.run(arena, small, O.MODE_COMPUTE)
     assert np.array_equal(o2, want[:cut])
     g.close()
+
+
+def test_survey_entry_points_over_the_default_group(orc):
+    """vpcsum_init(dev_mask) / vpcsum_register_arena / vpcsum_batch_submit / vpcsum_batch_wait /
+    vpcsum_nat_submit / vpcsum_shutdown: a checksum batch and a NAT batch over
+    the process-wide group, results equal to the oracle's; a second init is refused."""
+    import ctypes
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import oracle as O
+    from vproxy_amd import vpcsum as V
+    L = V.lib()
+    mask = (1 << torch.cuda.device_count()) - 1
+    arena, d = orc.synth(3000, 2048, 14, O.SYNTH_C3, O.SEED, 4321)
+    arena = np.concatenate([arena, np.zeros(4096, np.uint8)])
+    want_out, want_st = orc.process(arena, d, O.MODE_VERIFY)
+    assert L.vpcsum_init(mask, arena.nbytes, len(d)) == 0
+    try:
+        assert L.vpcsum_init(mask, arena.nbytes, len(d)) != 0
+        assert L.vpcsum_register_arena(arena.ctypes.data, arena.nbytes) == 0
+        out, st = np.zeros(len(d), np.uint32), np.zeros(len(d), np.uint8)
+        h = ctypes.c_uint64()
+        assert L.vpcsum_batch_submit(arena.ctypes.data, arena.nbytes, d.ctypes.data, len(d), out.ctypes.data,
+                                     st.ctypes.data, O.MODE_VERIFY, ctypes.byref(h)) == 0
+        assert L.vpcsum_batch_wait(h.value) == 0
+        assert np.array_equal(out, want_out) and np.array_equal(st, want_st)
+        # NAT over the group: valid sums first, then rewrites, equal to Java's setters + recompute
+        orc.process(arena, d, O.MODE_COMPUTE, write=True)
+        rng = np.random.default_rng(9)
+        rw = np.zeros(len(d), O.NAT_DTYPE)
+        rw["src"][:, :4] = rng.integers(0, 256, (len(d), 4))
+        rw["dport"] = rng.integers(0, 256, (len(d), 2))
+        rw["mask"] = O.NAT_SRC | O.NAT_DPORT
+        want = arena.copy()
+        want_nst = orc.nat_java(want, d, rw)
+        nst = np.zeros(len(d), np.uint8)
+        assert L.vpcsum_nat_submit(arena.ctypes.data, arena.nbytes, d.ctypes.data, rw.ctypes.data, len(d),
+                                   nst.ctypes.data, V.NAT_STRICT_JAVA, ctypes.byref(h)) == 0
+        assert L.vpcsum_batch_wait(h.value) == 0
+        assert np.array_equal(arena, want) and np.array_equal(nst, want_nst)
+    finally:
+        assert L.vpcsum_shutdown() == 0

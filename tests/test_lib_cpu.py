@@ -90,3 +90,20 @@ def test_pni_env_layout_and_errno(libpath, tmp_path):
                            "-lvpcsum", "-Wl,-rpath," + os.path.dirname(libpath), "-o", str(exe)])
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "pni layout ok" in r.stdout, (r.returncode, r.stdout, r.stderr)
+
+
+def test_survey_entry_points_refuse_before_init(libpath):
+    """SURVEY.md §8(b)'s names (vpcsum_init / vpcsum_batch_submit / vpcsum_batch_wait /
+    vpcsum_nat_submit) work over one process-wide group; before vpcsum_init every one of them
+    fails with a message instead of touching a device (no GPU call here)."""
+    L = ctypes.CDLL(libpath)
+    L.vpcsum_last_error.restype = ctypes.c_char_p
+    h = ctypes.c_uint64()
+    assert L.vpcsum_batch_submit(None, ctypes.c_uint64(0), None, ctypes.c_uint32(0), None, None,
+                                 ctypes.c_uint32(0), ctypes.byref(h)) != 0
+    assert b"vpcsum_init first" in L.vpcsum_last_error()
+    assert L.vpcsum_batch_wait(ctypes.c_uint64(1)) != 0
+    assert L.vpcsum_nat_submit(None, ctypes.c_uint64(0), None, None, ctypes.c_uint32(0), None,
+                               ctypes.c_uint32(0), ctypes.byref(h)) != 0
+    assert L.vpcsum_register_arena(None, ctypes.c_uint64(0)) != 0
+    assert L.vpcsum_shutdown() == 0   # nothing to shut down: a no-op

@@ -1233,15 +1233,18 @@ int vpcsum_group_unregister_arena(vpcsum_group_t* g, void* h_arena) {
     return 0;
 }
 
-int vpcsum_group_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
-                        uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket) {
-    if (!g || !ticket) return fail("vpcsum_group_submit: NULL group or ticket");
-    if (n && (!h_arena || !h_desc)) return fail("vpcsum_group_submit: NULL arena or descriptors");
-    std::lock_guard<std::mutex> lk(g->mu);
+}  // extern "C"
+
+// Byte-balanced contiguous cuts of a host batch over the group's contexts (shard_by_bytes in
+// vproxy_amd/shard.py); submit(d, a, b, &ticket) hands range [a, b) to context d.  A range a
+// context refuses fails the group submit only after the ranges already submitted have finished:
+// they write into the caller's buffers, which the caller may free once the error is back.
+template <class Submit>
+static int group_submit_ranges(vpcsum_group* g, const vpcsum_desc_t* h_desc, uint32_t n, uint64_t* ticket,
+                               Submit submit) {
     const uint64_t t = g->next_ticket++;
     auto& slot = g->slots[t & 1];
     if (slot.ticket && vpcsum_group_wait_locked(g, slot) != 0) return -1;
-    // byte-balanced contiguous cuts (shard_by_bytes in vproxy_amd/shard.py)
     const size_t k = g->ctx.size();
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i) total += h_desc[i].l3_len;
@@ -1256,10 +1259,7 @@ int vpcsum_group_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len,
     slot.sub.assign(k, 0);
     for (size_t d = 0; d < k; ++d) {
         const uint32_t a = cut[d], b = std::max(cut[d], cut[d + 1]);
-        if (vpcsum_ctx_submit(g->ctx[d], h_arena, arena_len, h_desc + a, b - a, h_out ? h_out + a : nullptr,
-                              h_status ? h_status + a : nullptr, mode, &slot.sub[d]) != 0) {
-            // the ranges already submitted write into the caller's buffers when they finish:
-            // join them before reporting the failure, so the caller may free its buffers
+        if (submit(d, a, b, &slot.sub[d]) != 0) {
             const std::string e = g_err;
             for (size_t q = 0; q < d; ++q) (void)vpcsum_ctx_wait(g->ctx[q], slot.sub[q]);
             slot.sub.clear();
@@ -1271,6 +1271,31 @@ int vpcsum_group_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len,
     return 0;
 }
 
+extern "C" {
+
+int vpcsum_group_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                        uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket) {
+    if (!g || !ticket) return fail("vpcsum_group_submit: NULL group or ticket");
+    if (n && (!h_arena || !h_desc)) return fail("vpcsum_group_submit: NULL arena or descriptors");
+    std::lock_guard<std::mutex> lk(g->mu);
+    return group_submit_ranges(g, h_desc, n, ticket, [&](size_t d, uint32_t a, uint32_t b, uint64_t* t) {
+        return vpcsum_ctx_submit(g->ctx[d], h_arena, arena_len, h_desc + a, b - a, h_out ? h_out + a : nullptr,
+                                 h_status ? h_status + a : nullptr, mode, t);
+    });
+}
+
+int vpcsum_group_nat_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                            const vpcsum_nat_t* h_rw, uint32_t n, uint8_t* h_status, uint32_t nat_mode,
+                            uint64_t* ticket) {
+    if (!g || !ticket) return fail("vpcsum_group_nat_submit: NULL group or ticket");
+    if (n && (!h_arena || !h_desc || !h_rw)) return fail("vpcsum_group_nat_submit: NULL arena, descriptors or rewrites");
+    std::lock_guard<std::mutex> lk(g->mu);
+    return group_submit_ranges(g, h_desc, n, ticket, [&](size_t d, uint32_t a, uint32_t b, uint64_t* t) {
+        return vpcsum_ctx_nat_submit(g->ctx[d], h_arena, arena_len, h_desc + a, h_rw + a, b - a,
+                                     h_status ? h_status + a : nullptr, nat_mode, t);
+    });
+}
+
 int vpcsum_group_wait(vpcsum_group_t* g, uint64_t ticket) {
     if (!g) return fail("vpcsum_group_wait: NULL group");
     std::lock_guard<std::mutex> lk(g->mu);
@@ -1280,6 +1305,56 @@ int vpcsum_group_wait(vpcsum_group_t* g, uint64_t ticket) {
         return 0;   // already completed
     }
     return vpcsum_group_wait_locked(g, slot);
+}
+
+// SURVEY.md §8(b)'s entry points over one process-wide device group (vpcsum_init creates it).
+// vpcsum_shutdown must not race a submit or wait of another thread: the caller quiesces first,
+// as with vpcsum_group_destroy.
+static std::mutex g_default_mu;
+static vpcsum_group* g_default = nullptr;
+
+static vpcsum_group* default_group(const char* what) {
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    if (!g_default) fail("%s: vpcsum_init first", what);
+    return g_default;
+}
+
+int vpcsum_init(uint64_t dev_mask, uint64_t max_arena_bytes, uint32_t max_pkts) {
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    if (g_default) return fail("vpcsum_init: already initialised (vpcsum_shutdown first)");
+    vpcsum_group_t* g = nullptr;
+    if (vpcsum_group_create(dev_mask, max_arena_bytes, max_pkts, &g) != 0) return -1;
+    g_default = g;
+    return 0;
+}
+
+int vpcsum_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    vpcsum_group_t* g = g_default;
+    g_default = nullptr;
+    return vpcsum_group_destroy(g);
+}
+
+int vpcsum_register_arena(void* h_arena, uint64_t len) {
+    vpcsum_group* g = default_group("vpcsum_register_arena");
+    return g ? vpcsum_group_register_arena(g, h_arena, len) : -1;
+}
+
+int vpcsum_batch_submit(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, uint32_t n,
+                        uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* handle) {
+    vpcsum_group* g = default_group("vpcsum_batch_submit");
+    return g ? vpcsum_group_submit(g, h_arena, arena_len, h_desc, n, h_out, h_status, mode, handle) : -1;
+}
+
+int vpcsum_nat_submit(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, const vpcsum_nat_t* h_rw,
+                      uint32_t n, uint8_t* h_status, uint32_t nat_mode, uint64_t* handle) {
+    vpcsum_group* g = default_group("vpcsum_nat_submit");
+    return g ? vpcsum_group_nat_submit(g, h_arena, arena_len, h_desc, h_rw, n, h_status, nat_mode, handle) : -1;
+}
+
+int vpcsum_batch_wait(uint64_t handle) {
+    vpcsum_group* g = default_group("vpcsum_batch_wait");
+    return g ? vpcsum_group_wait(g, handle) : -1;
 }
 
 // ------------------------------------------------------------------------------------------

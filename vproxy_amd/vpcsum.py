@@ -47,7 +47,9 @@ EXPORTS = [
     "vpcsum_ctx_parse_frames", "vpcsum_ctx_egress_frames", "Java_io_vproxy_vpcsum_VPCsum_egressFrames",
     "vpcsum_ctx_nat_submit", "Java_io_vproxy_vpcsum_VPCsum_natSubmit",
     "vpcsum_group_create", "vpcsum_group_create_list", "vpcsum_group_destroy", "vpcsum_group_register_arena",
-    "vpcsum_group_unregister_arena", "vpcsum_group_submit", "vpcsum_group_wait",
+    "vpcsum_group_unregister_arena", "vpcsum_group_submit", "vpcsum_group_wait", "vpcsum_group_nat_submit",
+    "vpcsum_init", "vpcsum_shutdown", "vpcsum_register_arena", "vpcsum_batch_submit", "vpcsum_nat_submit",
+    "vpcsum_batch_wait",
     "Java_io_vproxy_vpcsum_VPCsum_create", "Java_io_vproxy_vpcsum_VPCsum_registerArena",
     "Java_io_vproxy_vpcsum_VPCsum_submit", "Java_io_vproxy_vpcsum_VPCsum_waitFor",
     "Java_io_vproxy_vpcsum_VPCsum_close", "Java_io_vproxy_vpcsum_VPCsum_setService",
@@ -85,6 +87,13 @@ def _declare(L):
         "vpcsum_group_unregister_arena": ([P, P], I),
         "vpcsum_group_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
         "vpcsum_group_wait": ([P, U64], I),
+        "vpcsum_group_nat_submit": ([P, P, U64, P, P, U32, P, U32, P], I),
+        "vpcsum_init": ([U64, U64, U32], I),
+        "vpcsum_shutdown": ([], I),
+        "vpcsum_register_arena": ([P, U64], I),
+        "vpcsum_batch_submit": ([P, U64, P, U32, P, P, U32, P], I),
+        "vpcsum_nat_submit": ([P, U64, P, P, U32, P, U32, P], I),
+        "vpcsum_batch_wait": ([U64], I),
         "vpcsum_parse_ether_async": ([P, U64, P, P, U32, U8, P, P, P], I),
         "vpcsum_parse_ether_tuples_async": ([P, U64, P, P, U32, U8, P, P, P, P], I),
         "vpcsum_read_probe_async": ([P, U64, P, U32, P], I),
@@ -409,6 +418,17 @@ class Group:
                                          out.ctypes.data, None if status is None else status.ctypes.data, mode,
                                          ctypes.byref(t)), "vpcsum_group_submit")
         self._inflight[t.value & 1] = (arena, desc, out, status)
+        return t.value
+
+    def nat_submit(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray, status: np.ndarray | None = None,
+                   nat_mode: int = NAT_RFC1624) -> int:
+        """NAT / TTL rewrites of host frames cut over the group's devices (vpcsum_group_nat_submit)."""
+        assert rw.dtype == NAT_DTYPE and len(rw) >= len(desc)
+        t = ctypes.c_uint64()
+        _check(lib().vpcsum_group_nat_submit(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data,
+                                             rw.ctypes.data, len(desc), None if status is None else status.ctypes.data,
+                                             nat_mode, ctypes.byref(t)), "vpcsum_group_nat_submit")
+        self._inflight[t.value & 1] = (arena, desc, rw, status)
         return t.value
 
     def wait(self, ticket: int):
