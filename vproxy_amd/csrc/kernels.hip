@@ -41,6 +41,7 @@ constexpr int kSmallUnroll = 2;
 // without it, all waves read the same offset within their units at the same moment, and the
 // HBM channel/bank mapping aliases those addresses: C2 -4%.
 constexpr int kDefaultRot = -9;
+constexpr int kEsUnits = 8;   // K2 (DS): units whose out / status words a wave stages in LDS
 
 // Sum over the TEAM lanes of a team (aligned lane groups; every lane gets the total).  Teams of
 // up to 16 lanes reduce with DPP lane swizzles inside a row (xor 1, xor 2 by quad_perm, then
@@ -620,7 +621,7 @@ __device__ __forceinline__ uint4 win_sums(const uint32_t (&x)[20], int sh, int v
 // k_csum_service: the persistent service grid, once per batch).
 // ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
 // ROT > 0 rotates whole iterations (64 / TEAM packets), ROT < 0 single slots.
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false>
 __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -671,6 +672,33 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     // the back edge (this unit's stores pending) would have to honour too
     asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    // DS: on a batch the sample found to hold large packets (the low-concurrency grid: few,
+    // long-lived waves), the out / status words of up to kEsUnits units wait in LDS and are stored
+    // together when the wave's staging is full and when it leaves, instead of cutting into the
+    // stream of packet reads once per unit.  Other batches (small and
+    // mixed packets: short-lived waves, nothing to batch) and waves of fewer than 4 units (C4's
+    // 2 per wave: -0.3%) store each unit's words at once.
+    const bool stage = DS && grid < gdim && n / 4u >= wstride;
+    __shared__ uint32_t s_eo[4][DS ? kEsUnits : 1][64];
+    __shared__ uint8_t s_es[4][DS ? kEsUnits : 1][64];
+    uint32_t es_n = 0, es_P0 = P0;
+    auto es_flush = [&]() {
+        uint32_t ln = lo;
+        asm volatile("" : "+v"(ln));
+        for (uint32_t k = 0; k < es_n; ++k) {
+            const uint32_t p = es_P0 + k * wstride + ln;
+            if (p < n) {
+                if (NT) {
+                    if (out) __builtin_nontemporal_store(s_eo[wid][k][lane], (__attribute__((address_space(1))) uint32_t*)(out + p));
+                    if (status) __builtin_nontemporal_store(s_es[wid][k][lane], (__attribute__((address_space(1))) uint8_t*)(status + p));
+                } else {
+                    if (out) out[p] = s_eo[wid][k][lane];
+                    if (status) status[p] = s_es[wid][k][lane];
+                }
+            }
+        }
+        es_n = 0;
+    };
     for (uint32_t Pn; P0 < n; P0 = Pn) {
         // ---- phase A: this lane's packet ----
         const uint4 dv = dnext;
@@ -811,13 +839,16 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                             }
                         }
                         asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
+                        const uint32_t res_out = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
                         if (arena_w) {
                             uint8_t* w = arena_w + off;
                             if (ur.do_ip) st_be16_nt(w + 10, ipc);
                             if (ur.do_l4) st_be16_nt(w + u_l4o2 + ur.fld, l4c);
                         }
-                        const uint32_t res_out = (ipc & 0xffff) | ((l4c & 0xffff) << 16);
-                        if (NT) {
+                        if (DS && stage) {
+                            s_eo[wid][es_n][lane] = res_out;
+                            s_es[wid][es_n][lane] = (uint8_t)st;
+                        } else if (NT) {
                             if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lo));
                             if (status) __builtin_nontemporal_store((uint8_t)st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lo));
                         } else {
@@ -952,7 +983,10 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                     res_st = st;
                 }
             }
-            if (live) {
+            if (DS && stage) {
+                s_eo[wid][es_n][lane] = res_out;
+                s_es[wid][es_n][lane] = (uint8_t)res_st;
+            } else if (live) {
                 if (NT) {
                     if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lo));
                     if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lo));
@@ -988,16 +1022,21 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         }
         if (!fastu) finish(sums);
         wave_sync_lds();   // slots are rewritten by the next super-iteration
+        if (DS && stage && ++es_n == kEsUnits) {
+            es_flush();
+            es_P0 = Pn;
+        }
     }
+    if (DS && stage) es_flush();
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
                                                 uint8_t* __restrict__ arena_w, uint32_t low_grid) {
-    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT>(arena, arena_len, desc, n, out, status, flags_override, arena_w,
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS>(arena, arena_len, desc, n, out, status, flags_override, arena_w,
                                                 low_grid, blockIdx.x, gridDim.x);
 }
 
@@ -1216,7 +1255,7 @@ static uint32_t default_low_grid() {
     return (uint32_t)num_cus(dev) * 2u;
 }
 
-template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, bool adapt, hipStream_t stream) {
@@ -1239,7 +1278,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     const uint32_t cus = (uint32_t)num_cus(dev);
 #define VPC_LAUNCH(V, N)                                                                                         \
     do {                                                                                                         \
-        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT>;                                       \
+        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT, DS>;                                       \
         uint32_t gg = g;                                                                                         \
         if (dense) {                                                                                             \
             static const uint32_t res = resident_wgs((const void*)kern);                                         \
@@ -1302,8 +1341,10 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         // 70: the default; 72: the default without window units (A/B)
         case 72: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 74: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        // 76: the default without staged result stores (A/B)
+        case 76: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 70:
-        case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         default: return hipErrorInvalidValue;   // unknown kernel variant id
     }
 #undef VPC_T
