@@ -367,7 +367,7 @@ def main():
     # measured read ceilings (context for the roofline fraction)
     sink = torch.zeros(8192, dtype=torch.int32, device="cuda")
     e0, e1 = V.Event(), V.Event()
-    read_ceiling = pattern_ceiling = None
+    read_ceiling = pattern_ceiling = unit_order_ceiling = None
     if not nat and n:
         span = arena_all[int(desc_np["l3_off"].min()) // 16 * 16:]   # every batch of the rotation
         for _ in range(3):
@@ -391,6 +391,19 @@ def main():
                 e1.record(stream)
                 pms.append(e0.elapsed_ms(e1) / 10)
             pattern_ceiling = bytes_per_step / (min(pms) * 1e-3) / 1e9
+            # the same reads in K2's packet order (a wave walks its own 64 consecutive packets,
+            # grid-strided units): the order costs C3 ~9% against the grid order above (DESIGN.md
+            # §5 item 24), so the kernel is also reported against this one
+            pus = []
+            for bpc in (5, 12):
+                for _ in range(3):
+                    V.pattern_probe(arena, d, n, sink, (cus * bpc) | (1 << 31), stream=stream)
+                e0.record(stream)
+                for _ in range(10):
+                    V.pattern_probe(arena, d, n, sink, (cus * bpc) | (1 << 31), stream=stream)
+                e1.record(stream)
+                pus.append(e0.elapsed_ms(e1) / 10)
+            unit_order_ceiling = bytes_per_step / (min(pus) * 1e-3) / 1e9
     elif nat and n:
         # NAT's own memory operations with no rewrite (vpcsum_nat4_pattern_probe_async: descriptor
         # and entry reads, the header window loads, the one store of [L3+10, checksum end)),
@@ -491,7 +504,9 @@ def main():
                 "measured_read_ceiling_GBps": round(read_ceiling, 1) if read_ceiling else None,
                 "measured_pattern_ceiling_GBps": round(pattern_ceiling, 1) if pattern_ceiling else None,
                 "frac_of_pattern_ceiling": round(achieved / pattern_ceiling, 4) if pattern_ceiling else None,
-                "pattern_ceiling_kernel": ("k_natw probe (same loads and stores, no rewrite)" if nat else
+                "measured_unit_order_ceiling_GBps": round(unit_order_ceiling, 1) if unit_order_ceiling else None,
+                "frac_of_unit_order_ceiling": round(achieved / unit_order_ceiling, 4) if unit_order_ceiling else None,
+                "pattern_ceiling_kernel": ("k_natq probe (same loads and stores, no rewrite)" if nat else
                                            "k_pattern_probe (K2's chunk reads, no checksum work)")
                 if pattern_ceiling else None,
                 "traffic_over_algorithmic": round(traffic / bytes_per_step, 3) if traffic and bytes_per_step else None,

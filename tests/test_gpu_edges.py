@@ -244,6 +244,7 @@ def test_nat_edges(V, orc, packets, pad):
     forced = [int.from_bytes(want[int(d["l3_off"]) + int(d["l4_off"]) + O.L4_FIELD[int(d["l4_proto"])]:][:2].tobytes(), "big")
               for d in desc[::2]]
     assert set(forced) <= {0, 0xFFFF} and 0 in forced and 0xFFFF in forced
-    for mode in (0, 0x100, V.NAT_STRICT_JAVA, V.NAT_STRICT_JAVA | 0x100):
+    # 0x800000: the lane-layout wide kernel (k_natw) instead of the default quads (k_natq)
+    for mode in (0, 0x100, 0x800000, V.NAT_STRICT_JAVA, V.NAT_STRICT_JAVA | 0x100, V.NAT_STRICT_JAVA | 0x800000):
         got, st = _gpu_nat(V, arena, desc, rw, mode)
         assert np.array_equal(got, want), hex(mode)

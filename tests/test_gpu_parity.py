@@ -264,9 +264,10 @@ def test_nat_wide_and_scalar_kernels(V, orc, pad, workload, packed):
     assert set(np.unique(want_st[v4])) <= {O.S_DONE, O.S_BAD_DESC | O.S_TTL_EXPIRED}
     # default, byte-access kernel (bit 8), wide kernel with 1 / 2 / 4 packets per lane (bits 12..14),
     # 4- and 6-chunk windows (bits 16..17: packets that do not fit 4 take the byte path), grids of
-    # 3 and 16 workgroups per CU (bits 18..22)
+    # 3 and 16 workgroups per CU (bits 18..22); the lane layout (k_natw, bit 23) next to the default
+    # quads (k_natq), and quads under a waves-per-EU bound of 6 / 8 (bits 24..25)
     for force_scalar in (0, 0x100, 0x1000, 0x2000, 0x3000, 0x10000, 0x20000, 0x23000, 0x20000 | (3 << 18),
-                         0x20000 | (16 << 18)):
+                         0x20000 | (16 << 18), 0x800000, 0x801000, 0x823000, 0x1021000, 0x2002000):
         got, st = _gpu_nat(V, arena, desc, rw, V.NAT_RFC1624 | force_scalar)
         assert np.array_equal(st, want_st), force_scalar
         assert np.array_equal(got, want), force_scalar
@@ -741,6 +742,47 @@ def test_low_concurrency_grid(V, orc):
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy().view(np.uint32), want), full
         assert np.array_equal(st.cpu().numpy(), want_st), full
+
+
+def test_staged_result_stores(V, orc):
+    """Large-packet batches big enough that every wave of the low-concurrency grid takes >= 4
+    units stage their out / status words in LDS: n is not a multiple of 64
+    (a partial last unit), some descriptors are bad, some packets small, one raw range; verify
+    mode (out + status), compute mode (out only), and write mode (checksum fields in place, the
+    words staged) all equal the oracle's, and the default equals variant 76 (no staging)."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = 4 * (cus * 2 * 256) + 9000 + 37          # >= 4 units per wave of the 2-WG/CU grid
+    a, d = orc.synth(n, 2048, 0, O.SYNTH_C2, O.SEED, 77)
+    sampled = {(n * lane) >> 6 for lane in range(64)}
+    rng = np.random.default_rng(77)
+    pick = np.array(sorted(set(rng.choice(n, 4000, replace=False).tolist()) - sampled))
+    d = d.copy()
+    d["l3_len"][pick[:1500]] = 64                  # small packets the sample did not see
+    d["l3_len"][pick[1500:2000]] = 0               # bad: shorter than an IPv4 header
+    d["l3_off"][pick[2000:2300]] = a.size + 4096   # bad: outside the arena
+    d["flags"][pick[2300:2400]] = O.F_RAW          # raw ranges
+    want, want_st = orc.process(a, d, O.MODE_VERIFY, threads=8)
+    arena = dev(a)
+    dt = V.desc_to_tensor(d)
+    for team in (0, 76):
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        V.compute(arena, dt, n, out, st, O.MODE_VERIFY, team)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want), team
+        assert np.array_equal(st.cpu().numpy(), want_st), team
+        out.zero_()
+        V.compute(arena, dt, n, out, None, O.MODE_COMPUTE, team)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want), team
+    # write mode: the fields land in the frames (direct stores), the words are staged
+    w_out, _ = orc.process(a, d, O.MODE_COMPUTE, write=True)   # a now holds the written frames
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    V.compute(arena, dt, n, out, None, O.MODE_WRITE, 0)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), w_out)
+    assert np.array_equal(arena.cpu().numpy(), a)
 
 
 # ---- low-latency service (persistent grid polling a pinned mailbox) ----

@@ -248,8 +248,9 @@ static int nat_async(const char* what, uint8_t* d_arena, uint64_t arena_len, con
     if (n == 0) return 0;
     if (!d_arena || !d_desc || !d_rw) return fail("%s: NULL arena, descriptors or rewrite table", what);
     // tuning hints (not part of the stable ABI): bit 8 byte-access kernel, bits 12..14 packets
-    // per lane of the wide kernel, bits 16..17 window chunks, bits 18..22 workgroups per CU
-    if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u | 0x7000u | 0x7f0000u)) return fail("%s: bad nat_mode 0x%x", what, nat_mode);
+    // per lane of the wide kernel, bits 16..17 window chunks, bits 18..22 workgroups per CU, bit 23
+    // the lane layout of the wide kernel instead of quads
+    if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u | 0x7000u | 0x3ff0000u)) return fail("%s: bad nat_mode 0x%x", what, nat_mode);
     if ((nat_mode & VPCSUM_NAT_STRICT_JAVA) && !d_status) return fail("%s: strict-java mode needs a status buffer", what);
     return nat_run(d_arena, arena_len, d_desc, d_rw, fmt, n, d_status, nat_mode, (hipStream_t)stream);
 }

@@ -15,7 +15,8 @@
 // recomputes in full: identical to Java for any input.
 //
 // Two rewrite-entry formats: vpcsum_nat4_t (16 B, IPv4 only: BASELINE config C5's 72 B/packet)
-// and vpcsum_nat_t (48 B, IPv4 and IPv6).  One lane per packet.
+// and vpcsum_nat_t (48 B, IPv4 and IPv6).  One lane per packet for the rewrite; the default wide
+// kernel (k_natq) moves the header windows in and out by quads of lanes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -418,6 +419,199 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
     }
 }
 
+// Store bytes [s, e) of window chunk c (window coordinates; bytes before r0 and at or past lim are
+// not the packet's and are left alone) from the packet's LDS slot to base + 16c: the whole chunk
+// as one dwordx4 when it lies inside the packet (its unchanged bytes rewritten with their own
+// values), else dwordx2 / dword pieces, bytes only at the packet end.
+__device__ __forceinline__ void natq_store_chunk(uint8_t* base, const uint32_t* slot, int c, int s, int e, int lim,
+                                                 int r0) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(1))) uint32_t g32;
+    const int cs = max(s, 16 * c), ce = min(e, 16 * c + 16);
+    if (ce <= cs) return;
+    int j = cs >> 2;
+    const int je = (ce + 3) >> 2;
+    const int jfull = lim >> 2;   // dwords below this lie inside the packet
+    if (16 * c >= r0 && 16 * c + 16 <= lim) {
+        const uint32_t* q = slot + 4 * c;
+        *(__attribute__((address_space(1))) v4u*)(base + 16 * c) = v4u{q[0], q[1], q[2], q[3]};
+        return;
+    }
+    while (j < je) {
+        uint8_t* dst = base + 4 * j;
+        if (!(j & 1) && j + 2 <= je && j + 2 <= jfull) {
+            *(__attribute__((address_space(1))) v2u*)dst = v2u{slot[j], slot[j + 1]};
+            j += 2;
+        } else if (j + 1 <= jfull) {
+            *(g32*)dst = slot[j];
+            j += 1;
+        } else {
+            const uint8_t* wb = (const uint8_t*)slot;
+            for (int q = 4 * j; q < lim; ++q) base[q] = wb[q];
+            j += 1;
+        }
+    }
+}
+
+// Quad form of k_natw: the same per-lane rewrite on an LDS window, but the wave's header windows
+// are loaded and stored back by quads -- lane L moves chunk L & 3 of packet 16u + (L >> 2) in
+// instruction u -- so one vector-memory instruction touches 16 frames' lines instead of 64.  The
+// NAT access pattern (one 128-B line read and a 32..64-B write per 2-KB frame) measured 20.5 vs
+// 24.9 Gframes/s for the two layouts (tools/bwlab.hip nat).  Windows of more than
+// 4 chunks (IPv4 options, IPv6: CH = 6) take a second quad round when any packet of the wave needs
+// it.  The loop is wave-uniform: every lane takes part in the quad moves.
+template <int FMT, bool STRICT, int W, bool PROBE = false, int CH = kNatChunks, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_natq(uint8_t* __restrict__ arena, uint64_t arena_len,
+                                             const uint4* __restrict__ desc, const void* __restrict__ rw, uint32_t n,
+                                             uint8_t* __restrict__ status, uint8_t* __restrict__ flags_out) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const v4u gv4u;
+    constexpr int kSlotDw = 4 * CH + 1;   // LDS slot per packet: an odd dword stride
+    constexpr int NR = (CH + 3) / 4;       // quad rounds per window
+    __shared__ uint32_t s_win[256 * kSlotDw];
+    const int lane = threadIdx.x & 63;
+    uint32_t* wsl = &s_win[(threadIdx.x & ~63u) * kSlotDw];   // this wave's 64 slots
+    uint32_t* slot = wsl + lane * kSlotDw;
+    uint8_t* w = (uint8_t*)slot;
+    const uint32_t T = gridDim.x * blockDim.x;
+    const int ql = lane & 3;
+    for (uint32_t p0w = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); p0w < n; p0w += W * T) {
+        const uint32_t p0 = p0w + (uint32_t)lane;
+        uint4 dv[W];
+        NatRw rr[W];
+        uint32_t blo[W], bhi[W];   // window base (16-B aligned absolute address)
+        int wend[W];               // bytes of the window this packet needs; 0: none (byte path / idle)
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            dv[i] = p < n ? desc[p] : make_uint4(0, 0, 0, 0);
+            rr[i] = nat_load_rw<FMT>(rw, p < n ? p : 0);
+        }
+        v4u v[W][4];   // quad round 0 (chunks 0..3); a second round, when a window needs it, is rare
+        bool r2[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
+            const int len = dv[i].z & 0xffff, l4o = dv[i].z >> 16;
+            const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
+            const bool ok = p < n && nat_desc_ok(off, len, l4o, ver, arena_len, FMT);
+            const uintptr_t la = ok ? (uintptr_t)(arena + off) : 0;
+            const int r0 = (int)(la & 15);
+            int need = ver == 4 ? 20 : 40;
+            if (nat_l4sum(ver, proto, len, l4o)) need = max(need, l4o + l4_field(proto) + 2);
+            wend[i] = ok && r0 + need <= 16 * CH ? r0 + need : 0;
+            const uint64_t base = (uint64_t)(la - (uintptr_t)r0);
+            blo[i] = (uint32_t)base;
+            bhi[i] = (uint32_t)(base >> 32);
+            r2[i] = NR > 1 && __ballot(wend[i] > 64) != 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = 16 * u + (lane >> 2);
+                const uint32_t ql_lo = (uint32_t)__shfl((int)blo[i], q, 64);
+                const uint32_t ql_hi = (uint32_t)__shfl((int)bhi[i], q, 64);
+                const int qe = __shfl(wend[i], q, 64);
+                v4u x = {0u, 0u, 0u, 0u};
+                // only the chunks the packet needs, inside its 16-B blocks (never past a page)
+                if ((ql << 4) < qe) x = *(gv4u*)((((uint64_t)ql_hi << 32) | ql_lo) + 16u * (uint32_t)ql);
+                v[i][u] = x;
+            }
+        }
+        uint32_t res[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            // stage the quads' chunks in the owners' slots
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                uint32_t* d = wsl + (16 * u + (lane >> 2)) * kSlotDw + 4 * ql;
+                d[0] = v[i][u].x; d[1] = v[i][u].y; d[2] = v[i][u].z; d[3] = v[i][u].w;
+            }
+            if (NR > 1 && r2[i]) {   // chunks 4.. of windows past 64 B (IPv4 options, IPv6)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int q = 16 * u + (lane >> 2);
+                    const uint32_t ql_lo = (uint32_t)__shfl((int)blo[i], q, 64);
+                    const uint32_t ql_hi = (uint32_t)__shfl((int)bhi[i], q, 64);
+                    const int qe = __shfl(wend[i], q, 64);
+                    const int k = 4 + ql;
+                    if (k < CH && (k << 4) < qe) {
+                        const v4u x = *(gv4u*)((((uint64_t)ql_hi << 32) | ql_lo) + 16u * (uint32_t)k);
+                        uint32_t* d = wsl + q * kSlotDw + 4 * k;
+                        d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            res[i] = 0;
+            // this lane's store range [s, e) in window coordinates and the packet end lim
+            int s = 0, e = 0, lim = 0;
+            bool udp_zero = false;
+            const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
+            const int len = dv[i].z & 0xffff, l4o = dv[i].z >> 16;
+            const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
+            if (p < n) {
+                if (!wend[i]) {
+                    if (!PROBE) res[i] = nat_scalar<FMT>(arena, arena_len, dv[i], rr[i], STRICT);
+                } else {
+                    const int r0 = (int)((uintptr_t)(arena + off) & 15);
+                    uint8_t* l3w = w + r0;
+                    lim = r0 + len;
+                    if (PROBE) {
+                        int hi = ver == 4 ? 20 : 40;
+                        if (nat_l4sum(ver, proto, len, l4o)) hi = max(hi, l4o + l4_field(proto) + 2);
+                        s = r0 + (ver == 4 ? 10 : 8);
+                        e = r0 + hi;
+                        res[i] = VPCSUM_S_DONE;
+                    } else if (nat_ttl_expired(l3w, ver, rr[i])) {
+                        res[i] = STRICT ? kFlagRejected : kNatExpired;
+                    } else {
+                        NatAcc a = nat_setters(l3w, ver, proto, len, l4o, nat_l4sum(ver, proto, len, l4o), rr[i]);
+                        if (!STRICT) udp_zero = nat_rfc1624(l3w, proto, l4o, l4_field(proto), a);
+                        if (a.hi > a.lo) { s = r0 + a.lo; e = r0 + a.hi; }
+                        res[i] = STRICT ? ((a.ip_dirty ? VPCSUM_F_IP : 0) | (a.l4_dirty ? VPCSUM_F_L4 : 0)) : VPCSUM_S_DONE;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            // the quads store the changed ranges back
+            // window coordinates are below 128: lim is clipped to a byte, r0 takes bits 24..27
+            const uint32_t rng = (uint32_t)s | ((uint32_t)e << 8) | ((uint32_t)min(lim, 255) << 16) |
+                                 ((uint32_t)(lim > 0 ? (int)((uintptr_t)(arena + off) & 15) : 0) << 24);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int q = 16 * u + (lane >> 2);
+                    const uint32_t qr = (uint32_t)__shfl((int)rng, q, 64);
+                    const uint32_t ql_lo = (uint32_t)__shfl((int)blo[i], q, 64);
+                    const uint32_t ql_hi = (uint32_t)__shfl((int)bhi[i], q, 64);
+                    const int k = 4 * r + ql;
+                    const int qs = (int)(qr & 0xff), qe = (int)((qr >> 8) & 0xff), qlim = (int)((qr >> 16) & 0xff);
+                    if (k < CH && qe > qs)
+                        natq_store_chunk((uint8_t*)(((uint64_t)ql_hi << 32) | ql_lo), wsl + q * kSlotDw, k, qs, qe, qlim,
+                                         (int)(qr >> 24));
+                }
+            }
+            if (!STRICT && !PROBE && __ballot(udp_zero)) {
+                // the quads' stores of the rewritten header before the owner reads it back
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                if (udp_zero) nat_udp_full(arena + off, ver, len, l4o);
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");   // the slots are rewritten for the next packet set
+        }
+        uint8_t* dst = STRICT ? flags_out : status;
+        if (dst) {
+#pragma unroll
+            for (int i = 0; i < W; ++i) store_bytes_packed(dst, p0 + i * T, n, res[i]);
+        }
+    }
+}
+
 // Strict mode's status after the recompute kernel: that kernel reports a refused packet as
 // S_BAD_DESC only, so the TTL-expired ones get their S_TTL_EXPIRED bit here, from the same test on
 // the same bytes: a refused packet was left untouched.  Only refused packets are looked at (a TTL
@@ -468,7 +662,7 @@ static uint32_t nat_grid(uint32_t n, int wl2, uint32_t wgs_per_cu) {
 
 // Internal tuning bits of nat_mode (not part of the stable ABI): bit 8 byte-access kernel; bits
 // 12..14 log2(packets per lane) + 1 of the wide kernel; bits 16..17 window chunks (1: 6, 2: 4);
-// bits 18..22 workgroups per CU (0: 24).
+// bits 18..22 workgroups per CU (0: 24); bit 23 the lane layout (k_natw) instead of quads (k_natq).
 static int nat_chunks_sel(uint32_t nat_mode, int fmt) {
     const uint32_t c = (nat_mode >> 16) & 3u;
     if (c == 1) return 6;
@@ -493,7 +687,17 @@ hipError_t launch_nat_probe(uint8_t* arena, uint64_t arena_len, const vpcsum_des
     const uint32_t g = nat_grid(n, kNatWideLog2, nat_wgs_per_cu(tune));
     const uint4* d = (const uint4*)desc;
     constexpr int W = 1 << kNatWideLog2;
-    if (fmt == 0 && nat_chunks_sel(tune, 0) == 4)
+    if (!(tune & 0x800000u)) {   // the quad layout (k_natq), as launch_nat's default
+        if (fmt == 0 && nat_chunks_sel(tune, 0) == 4)
+            hipLaunchKernelGGL((k_natq<0, false, W, true, 4>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n,
+                               (uint8_t*)nullptr, (uint8_t*)nullptr);
+        else if (fmt == 0)
+            hipLaunchKernelGGL((k_natq<0, false, W, true>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n,
+                               (uint8_t*)nullptr, (uint8_t*)nullptr);
+        else
+            hipLaunchKernelGGL((k_natq<1, false, W, true>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n,
+                               (uint8_t*)nullptr, (uint8_t*)nullptr);
+    } else if (fmt == 0 && nat_chunks_sel(tune, 0) == 4)
         hipLaunchKernelGGL((k_natw<0, false, W, true, 4>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n,
                            (uint8_t*)nullptr, (uint8_t*)nullptr);
     else if (fmt == 0)
@@ -514,8 +718,30 @@ hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d
     const uint32_t g = nat_grid(n, wl2, nat_wgs_per_cu(nat_mode));
     const int ch = nat_chunks_sel(nat_mode, fmt);
     const bool wide = !(nat_mode & 0x100u);
+    const bool quad = (nat_mode & 0x800000u) == 0;
     const uint4* d = (const uint4*)desc;
-    if (wide) {
+    if (wide && quad) {
+#define VPC_NATQ(F, S, W, C)                                                                                           \
+    do {                                                                                                               \
+        const uint32_t wpe = (nat_mode >> 24) & 3u;                                                                    \
+        if (wpe == 1)                                                                                                  \
+            hipLaunchKernelGGL((k_natq<F, S, W, false, C, 6>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out); \
+        else if (wpe == 2)                                                                                             \
+            hipLaunchKernelGGL((k_natq<F, S, W, false, C, 8>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out); \
+        else                                                                                                           \
+            hipLaunchKernelGGL((k_natq<F, S, W, false, C>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out); \
+    } while (0)
+#define VPC_NATQ_W(F, S, C) do { if (wl2 == 0) VPC_NATQ(F, S, 1, C); else VPC_NATQ(F, S, 2, C); } while (0)
+        if (fmt == 0 && ch == 4) {
+            if (strict) VPC_NATQ_W(0, true, 4); else VPC_NATQ_W(0, false, 4);
+        } else if (fmt == 0) {
+            if (strict) VPC_NATQ_W(0, true, kNatChunks); else VPC_NATQ_W(0, false, kNatChunks);
+        } else {
+            if (strict) VPC_NATQ_W(1, true, kNatChunks); else VPC_NATQ_W(1, false, kNatChunks);
+        }
+#undef VPC_NATQ_W
+#undef VPC_NATQ
+    } else if (wide) {
 #define VPC_NAT(F, S, W, C) hipLaunchKernelGGL((k_natw<F, S, W, false, C>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out)
 #define VPC_NAT_W(F, S) do { if (wl2 == 0) VPC_NAT(F, S, 1, kNatChunks); else if (wl2 == 1) VPC_NAT(F, S, 2, kNatChunks); else VPC_NAT(F, S, 4, kNatChunks); } while (0)
         if (fmt == 0 && !strict && ch == 4) {
