@@ -119,7 +119,7 @@ public final class GpuCsumBatch implements AutoCloseable {
 
     /**
      * Take over the dirty checksums of {@code pkb}, whose Ethernet frame lies in the umem at byte
-     * offset {@code frameOff} in {@code chunk} (the zero-copy branch of XDPIface.sendPacket:
+     * offset {@code frameAddr} in {@code chunk} (the zero-copy branch of XDPIface.sendPacket:
      * chunk.getAddr() + pkb.pktOff; the copying branch: the pktaddr the frame was copied to).
      * {@code nativeFlags} is what SwitchUtils.checksumFlagsFor (SwitchUtils.java:297-316) returned
      * for the packet: VP_CSUM_IP -> F_IP, VP_CSUM_UP -> F_L4, VP_CSUM_UP_PSEUDO -> F_L4P (the GPU
@@ -130,7 +130,7 @@ public final class GpuCsumBatch implements AutoCloseable {
      * (its full nativeFlags are restored on the chunk): a GPU round trip costs more than the CPU
      * there (DESIGN.md §8).
      */
-    public int defer(PacketBuffer pkb, ChunkInfo chunk, long frameOff, int nativeFlags) {
+    public int defer(PacketBuffer pkb, ChunkInfo chunk, long frameAddr, int nativeFlags) {
         if (nativeFlags == 0 || !(pkb.pkt.getPacket() instanceof AbstractIpPacket ip)) {
             return nativeFlags;
         }
@@ -155,7 +155,7 @@ public final class GpuCsumBatch implements AutoCloseable {
         if (n == capacity) {
             throw new IllegalStateException("batch full: flush first");
         }
-        long l3 = frameOff + (((EthernetPacket) pkb.pkt).getVlan() >= 0 ? 18 : 14);
+        long l3 = frameAddr + (((EthernetPacket) pkb.pkt).getVlan() >= 0 ? 18 : 14);
         // The lengths come from the IP header fields, never from the buffer: a frame parsed with
         // allowPartial (every XDP / tap frame, PacketBuffer.java:177 -> EthernetPacket.java:52-56)
         // keeps its Ethernet padding in pktBuf (Ipv4Packet.initPartial does not cut it,
