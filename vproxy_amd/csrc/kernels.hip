@@ -1343,8 +1343,16 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 74: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         // 76: the default without staged result stores (A/B)
         case 76: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        // 79: the staging build on every batch (round 3's r03w default, A/B)
+        case 79: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 70:
-        case 0: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 0:
+            // Dense small frames (at most 128 arena bytes per packet: C1) never stage their result
+            // words, and the staging build holds 92 VGPRs against 79 (5 resident waves per SIMD
+            // instead of 6): they take the build without staging
+            if (grid <= 0 && adapt && arena_len <= (uint64_t)n * 128u)
+                return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+            return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         default: return hipErrorInvalidValue;   // unknown kernel variant id
     }
 #undef VPC_T
