@@ -14,7 +14,9 @@ from tests.test_gpu_parity import V, gpu_compute  # noqa: F401  (V: the library 
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 72]
+# 0: the default (dense frames take the build without result staging);
+# 79: the staging build on the same batches; 72: K2 without window units
+VARIANTS = [0, 79, 72]
 
 # (ver, proto, l3_len, flags): shapes whose r0 + l3_len fits the first 64 B of the chunk-aligned
 # frame for r0 = 14 (l3_len <= 50) or r0 = 0 (<= 64)
