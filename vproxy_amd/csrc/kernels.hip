@@ -1240,9 +1240,10 @@ static uint32_t default_grid() {
     (void)hipGetDevice(&dev);
     return (uint32_t)num_cus(dev) * 12u;
 }
-// Grid of K2 for dense small frames: 5 workgroups per CU (all resident at 5 waves per SIMD).
-// Workgroups of one K2 build resident per CU (its VGPR and LDS use: 6 for the compute build at
-// 79 VGPRs, 5 for the verify build at 95), looked up once per build.
+// Grid of K2 for dense small frames: one resident round of the build launched.  Workgroups of
+// one K2 build resident per CU (its VGPR and LDS use: 6 for the unstaged compute build at 79
+// VGPRs, which dense frames take; 5 for the verify build at 95 and the staging build at 92),
+// looked up once per build.
 static uint32_t resident_wgs(const void* kern) {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, 0) != hipSuccess || nb <= 0) nb = 5;
