@@ -1018,9 +1018,12 @@ def test_l4_pseudo_partial_pcap(V, orc):
     assert partial == 12
 
 
-def test_arena_beyond_4gib(V, orc):
+@pytest.mark.parametrize("order", ["sorted", "shuffled"])
+def test_arena_beyond_4gib(V, orc, order):
     """Arenas past the 32-bit buffer-descriptor range (> 4 GiB, as a umem of a large switch can
-    be): packets below and above 4 GiB go through the global-load fallback, bit-exact."""
+    be): packets below and above 4 GiB, in address order and shuffled across the whole 5 GiB, go
+    through the team kernel's 64-bit loads, bit-exact."""
+    variant = 0
     import torch
     n, stride = 1500, 9216                                     # FUZZ frames reach 9000 B
     a, d = orc.synth(n, stride, 6, O.SYNTH_FUZZ, O.SEED, 4444)
@@ -1029,6 +1032,8 @@ def test_arena_beyond_4gib(V, orc):
     rng = np.random.default_rng(4)
     bases = np.sort(rng.choice(((5 << 30) - (1 << 20)) // 16384, n, replace=False)) * 16384 + 8
     bases[: n // 3] = np.arange(n // 3) * 16384 + 8          # a third below 4 GiB
+    if order == "shuffled":
+        rng.shuffle(bases)
     dg = d.copy()
     src = torch.from_numpy(a).cuda()
     for i in range(n):
@@ -1038,20 +1043,55 @@ def test_arena_beyond_4gib(V, orc):
     out = torch.zeros(n, dtype=torch.int32, device="cuda")
     st = torch.zeros(n, dtype=torch.uint8, device="cuda")
     dt = V.desc_to_tensor(dg)
-    V.compute(big, dt, n, out, st, O.MODE_VERIFY)
+    V.compute(big, dt, n, out, st, O.MODE_VERIFY, variant)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
     assert np.array_equal(st.cpu().numpy(), want_st)
     # in-place writes land at the right > 4 GiB addresses
     a2 = a.copy()
     orc.process(a2, d, O.MODE_COMPUTE, write=True)
-    V.compute(big, dt, n, out, None, O.MODE_WRITE)
+    V.compute(big, dt, n, out, None, O.MODE_WRITE, variant)
     torch.cuda.synchronize()
     for i in rng.choice(n, 64, replace=False):
         got = big[int(bases[i]): int(bases[i]) + stride].cpu().numpy()
         assert np.array_equal(got, a2[i * stride:(i + 1) * stride]), i
     del big
     torch.cuda.empty_cache()
+
+
+def test_batches_straddling_4gib(V, orc):
+    """Dense 64-B frames and C2 frames of one batch straddling the 4-GiB line of a large arena
+    (the team kernel's 64-bit loads), bit-exact with the oracle in compute,
+    verify and write-back."""
+    variant = 0
+    import torch
+    base = (4 << 30) - (64 << 10)
+    for sid, m, stride, pad in ((O.SYNTH_C1, 4096 + 37, 64, 14), (O.SYNTH_C2, 700, 2048, 0)):
+        a, d = orc.synth(m, stride, pad, sid, O.SEED, 77)
+        want, want_st = orc.process(a, d, O.MODE_COMPUTE)
+        big = torch.zeros(base + len(a) + 4096, dtype=torch.uint8, device="cuda")
+        big[base:base + len(a)] = torch.from_numpy(a).cuda()
+        dg = d.copy()
+        dg["l3_off"] += base
+        assert int(dg["l3_off"].min()) < (4 << 30) < int(dg["l3_off"].max())
+        dt = V.desc_to_tensor(dg)
+        out = torch.zeros(m, dtype=torch.int32, device="cuda")
+        st = torch.zeros(m, dtype=torch.uint8, device="cuda")
+        V.compute(big, dt, m, out, st, O.MODE_COMPUTE, variant)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+        assert np.array_equal(st.cpu().numpy(), want_st)
+        a2 = a.copy()
+        orc.process(a2, d, O.MODE_COMPUTE, write=True)
+        V.compute(big, dt, m, out, None, O.MODE_WRITE, variant)
+        torch.cuda.synchronize()
+        assert np.array_equal(big[base:base + len(a)].cpu().numpy(), a2)
+        V.compute(big, dt, m, out, st, O.MODE_VERIFY, variant)
+        torch.cuda.synchronize()
+        vo, vs = orc.process(a2.copy(), d, O.MODE_VERIFY)
+        assert np.array_equal(st.cpu().numpy(), vs)
+        del big
+        torch.cuda.empty_cache()
 
 
 def test_parse_rules_on_gpu(V, orc):

@@ -1344,6 +1344,8 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 74: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         // 76: the default without staged result stores (A/B)
         case 76: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        // 78: the team kernel with 64-bit loads, which serves arenas past 4 GiB (A/B, tooling)
+        case 78: return launch_team<kDefaultTeam, kDefaultUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid > 0 ? grid : (int)default_grid(), stream);
         // 79: the staging build on every batch (round 3's r03w default, A/B)
         case 79: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 70:
