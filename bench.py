@@ -404,7 +404,7 @@ def main():
                 e1.record(stream)
                 pus.append(e0.elapsed_ms(e1) / 10)
             unit_order_ceiling = bytes_per_step / (min(pus) * 1e-3) / 1e9
-        if nb > 1:
+        if nb > 2:
             # small-packet batches (C1): a batch is too small for a launch to reach the streaming
             # rate, so the kernel is also priced against a plain streaming read of the same number
             # of bytes per launch (one batch's frames + descriptors, contiguous), launched back to
