@@ -66,12 +66,14 @@ struct NatAcc {
     int lo, hi;
 };
 
-__device__ __forceinline__ void nat_word(uint8_t* w, int q, uint32_t mn, uint32_t& d1, uint32_t* d2) {
+// Overwrites the big-endian word at w[q] with mn; returns its RFC 1624 difference ~m + m'.  (The
+// callers add it to the sums it changes by value: a pointer into NatAcc put the struct in scratch
+// memory, 124 scratch accesses per packet set in k_natq)
+__device__ __forceinline__ uint32_t nat_word(uint8_t* w, int q, uint32_t mn) {
     const uint32_t m = ((uint32_t)w[q] << 8) | w[q + 1];
-    d1 += (~m & 0xffff) + mn;
-    if (d2) *d2 += (~m & 0xffff) + mn;
     w[q] = (uint8_t)(mn >> 8);
     w[q + 1] = (uint8_t)mn;
+    return (~m & 0xffff) + mn;
 }
 __device__ __forceinline__ void grow(NatAcc& a, int lo, int hi) {
     a.lo = min(a.lo, lo);
@@ -87,37 +89,44 @@ __device__ __forceinline__ NatAcc nat_setters(uint8_t* w, int ver, int proto, in
     // under IPv6; an ICMPv4 message has no pseudo header, so its sum does not change
     const bool addr_dirty = l4sum && (proto == 6 || proto == 17 || (ver == 6 && (proto == 58 || proto == 1)));
     const bool addr_sum = addr_dirty && proto != 1;
-    uint32_t* l4d = addr_sum ? &a.l4_diff : nullptr;
+    const uint32_t l4m = addr_sum ? 0xffffffffu : 0u;   // address differences into the L4 sum too
     if (ver == 4) {
         if (r.mask & VPCSUM_NAT_SRC) {
-            for (int k = 0; k < 2; ++k) nat_word(w, 12 + 2 * k, rw_word(r.src, k), a.ip_diff, l4d);
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t dd = nat_word(w, 12 + 2 * k, rw_word(r.src, k));
+                a.ip_diff += dd;
+                a.l4_diff += dd & l4m;
+            }
             a.ip_dirty = true; a.l4_dirty |= addr_dirty; a.l4_touch |= addr_sum;
             grow(a, 12, 16);
         }
         if (r.mask & VPCSUM_NAT_DST) {
-            for (int k = 0; k < 2; ++k) nat_word(w, 16 + 2 * k, rw_word(r.dst, k), a.ip_diff, l4d);
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t dd = nat_word(w, 16 + 2 * k, rw_word(r.dst, k));
+                a.ip_diff += dd;
+                a.l4_diff += dd & l4m;
+            }
             a.ip_dirty = true; a.l4_dirty |= addr_dirty; a.l4_touch |= addr_sum;
             grow(a, 16, 20);
         }
         if (r.mask & VPCSUM_NAT_SET_TTL) {   // setTtl(ttl)
-            nat_word(w, 8, ((uint32_t)r.ttl << 8) | w[9], a.ip_diff, nullptr);
+            a.ip_diff += nat_word(w, 8, ((uint32_t)r.ttl << 8) | w[9]);
             a.ip_dirty = true;
             grow(a, 8, 9);
         }
         if (r.mask & VPCSUM_NAT_DEC_TTL) {   // IPInputRoute: setTtl(ttl - 1)
-            nat_word(w, 8, ((uint32_t)((w[8] - 1) & 0xff) << 8) | w[9], a.ip_diff, nullptr);
+            a.ip_diff += nat_word(w, 8, ((uint32_t)((w[8] - 1) & 0xff) << 8) | w[9]);
             a.ip_dirty = true;
             grow(a, 8, 9);
         }
     } else {
-        uint32_t none = 0;
         if (r.mask & VPCSUM_NAT_SRC) {
-            for (int k = 0; k < 8; ++k) nat_word(w, 8 + 2 * k, rw_word(r.src, k), none, l4d);
+            for (int k = 0; k < 8; ++k) a.l4_diff += nat_word(w, 8 + 2 * k, rw_word(r.src, k)) & l4m;
             a.l4_dirty |= addr_dirty; a.l4_touch |= addr_sum;
             grow(a, 8, 24);
         }
         if (r.mask & VPCSUM_NAT_DST) {
-            for (int k = 0; k < 8; ++k) nat_word(w, 24 + 2 * k, rw_word(r.dst, k), none, l4d);
+            for (int k = 0; k < 8; ++k) a.l4_diff += nat_word(w, 24 + 2 * k, rw_word(r.dst, k)) & l4m;
             a.l4_dirty |= addr_dirty; a.l4_touch |= addr_sum;
             grow(a, 24, 40);
         }
@@ -126,12 +135,12 @@ __device__ __forceinline__ NatAcc nat_setters(uint8_t* w, int ver, int proto, in
     }
     if (l4sum && (proto == 6 || proto == 17)) {
         if (r.mask & VPCSUM_NAT_SPORT) {
-            nat_word(w, l4o, rw_word(&r.ports, 0), a.l4_diff, nullptr);
+            a.l4_diff += nat_word(w, l4o, rw_word(&r.ports, 0));
             a.l4_dirty = a.l4_touch = true;
             grow(a, l4o, l4o + 2);
         }
         if (r.mask & VPCSUM_NAT_DPORT) {
-            nat_word(w, l4o + 2, rw_word(&r.ports, 1), a.l4_diff, nullptr);
+            a.l4_diff += nat_word(w, l4o + 2, rw_word(&r.ports, 1));
             a.l4_dirty = a.l4_touch = true;
             grow(a, l4o + 2, l4o + 4);
         }
