@@ -425,8 +425,9 @@ def main():
                     t = e0.elapsed_ms(e1) / 50
                     if rep and (best is None or t < best[0]):
                         best = (t, bpc)
-            launch_read = {"bytes_per_launch": slab, "ms_per_launch": round(best[0], 5),
-                           "workgroups_per_cu": best[1], "GBps": round(slab / (best[0] * 1e-3) / 1e9, 1)}
+            if best is not None:
+                launch_read = {"bytes_per_launch": slab, "ms_per_launch": round(best[0], 5),
+                               "workgroups_per_cu": best[1], "GBps": round(slab / (best[0] * 1e-3) / 1e9, 1)}
     elif nat and n:
         # NAT's own memory operations with no rewrite (vpcsum_nat4_pattern_probe_async: descriptor
         # and entry reads, the header window loads, the one store of [L3+10, checksum end)),
