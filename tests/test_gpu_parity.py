@@ -563,6 +563,29 @@ def test_full_size_c2_properties(V, orc):
         assert o[i] == w[0]
 
 
+@pytest.mark.parametrize("cfg", ["c1", "c2", "c3", "c4"])
+def test_full_size_configs_equal_oracle(V, orc, cfg):
+    """Every BASELINE checksum config at its full size (C1 1,048,576 x 64-B frames, C2 1,048,576 x
+    1500 B, C3 1,048,576 mixed, C4 262,144 x 9000 B IPv6) through the default launch path, every
+    packet's result word equal to the oracle's (the bench's oracle gate, as a test)."""
+    import torch
+    sid, n, stride = {"c1": (O.SYNTH_C1, 1 << 20, 64), "c2": (O.SYNTH_C2, 1 << 20, 2048),
+                      "c3": (O.SYNTH_C3, 1 << 20, 2048), "c4": (O.SYNTH_C4, 1 << 18, 9216)}[cfg]
+    a, d = orc.synth(n, stride, 0, sid, O.SEED, 0)
+    want, want_st = orc.process(a, d, threads=8)
+    arena = torch.from_numpy(a).cuda()
+    dt = V.desc_to_tensor(d)
+    del a
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    V.compute(arena, dt, n, out, st, O.MODE_COMPUTE)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    del arena
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("team", [0, 3, 9, 40, 45, 46, 47])
 def test_packet_ending_at_unaligned_arena_end(V, orc, team):
     """Arena length not a multiple of 16 and the last packet ending exactly at the arena end:
