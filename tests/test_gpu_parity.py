@@ -582,6 +582,12 @@ def test_full_size_configs_equal_oracle(V, orc, cfg):
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
     assert np.array_equal(st.cpu().numpy(), want_st)
+    # the sums written into the frames, then verified: every requested sum checks out
+    V.compute(arena, dt, n, out, None, O.MODE_WRITE)
+    V.compute(arena, dt, n, None, st, O.MODE_VERIFY)
+    torch.cuda.synchronize()
+    want_ok = np.where(d["flags"] & O.F_IP, O.S_IP_OK, 0) | np.where(d["flags"] & O.F_L4, O.S_L4_OK, 0)
+    assert np.array_equal(st.cpu().numpy() & (O.S_IP_OK | O.S_L4_OK), want_ok.astype(np.uint8))
     del arena
     torch.cuda.empty_cache()
 
