@@ -170,19 +170,32 @@ def oracle_sample_gate(synth_id: int, stride: int, first: int, out_np: np.ndarra
             "sample_equal": bool(np.array_equal(out_np[off:off + m], want))}
 
 
-def pmc_traffic(tag: str, packets: int):
-    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC summary
+def pmc_traffic(tag: str, packets: int, profiles: str | None = None, src: str | None = None):
+    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 PMC summary
     (profiles/r*_pmc_<tag>/summary.json, tools/save_profiles.py: 2 x FETCH_SIZE + WRITE_SIZE, every
     read request being 128 B), scaled from the summary's packet count to this rank's `packets` (a
     strong shard holds part of the batch).  PMC counters cannot be read from inside this process,
-    so the value comes from that separate --pmc run of the same kernel and config."""
+    so the value comes from that separate --pmc run of the same kernel and config.
+
+    Which summary: one measured on the library sources this process runs (`src_hash` equal to
+    vproxy_amd/build.py:source_hash, the newest commit of those); when no summary matches, the
+    newest by commit time (never by tag name), reported as stale.  Returns (bytes, provenance)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{tag}", "summary.json")))
-    for f in reversed(files):
+    if src is None:
+        from vproxy_amd.build import source_hash
+        src = source_hash()
+    cands = []
+    for f in glob.glob(os.path.join(profiles or os.path.join(REPO, "profiles"), f"r*_pmc_{tag}", "summary.json")):
         d = json.load(open(f))
         if "hbm_bytes_per_launch" in d and d.get("packets"):
-            return int(round(d["hbm_bytes_per_launch"] * packets / d["packets"])), os.path.relpath(f, REPO)
-    return None, None
+            cands.append((d.get("src_hash") == src, d.get("head_time", 0), f, d))
+    if not cands:
+        return None, None
+    match = [c for c in cands if c[0]]
+    same, _, f, d = max(match or cands, key=lambda c: (c[1], c[2]))
+    return int(round(d["hbm_bytes_per_launch"] * packets / d["packets"])), {
+        "source": os.path.relpath(f, profiles or REPO) if profiles else os.path.relpath(f, REPO),
+        "head": d.get("head"), "src_hash": d.get("src_hash"), "stale": not same}
 
 
 def _free_port() -> int:
@@ -254,6 +267,7 @@ def main():
     torch.cuda.set_device(local % max(ndev, 1))
     from vproxy_amd import vpcsum as V
     from vproxy_amd.shard import all_ranks_ok, gather_over_ranks, max_over_ranks, shard_by_bytes, sum_over_ranks
+    from vproxy_amd.build import source_hash
     V.lib()
 
     synth_id, n_cfg, stride, desc_text = WORKLOADS[args.workload]
@@ -261,47 +275,49 @@ def main():
     strong = args.strong or nat
     stream = torch.cuda.current_stream()
     if strong:
-        # one global batch (the same bytes on every rank); this rank processes a byte-balanced slice
-        n_gen, first = n_cfg, 0
+        # one global batch, cut by bytes: the global descriptors alone give the cut, then this rank
+        # generates and holds only its own packets [lo, hi) of the global stream (a rank-sized
+        # arena, not the whole batch: C5's 10M x 2 KB would be 20.5 GB on every rank)
+        d_glob = torch.zeros(n_cfg * 16, dtype=torch.uint8, device="cuda")
+        V.synth(None, n_cfg, stride, 0, synth_id, SEED, 0, d_glob, stream=stream)
+        torch.cuda.synchronize()
+        lo, hi = shard_by_bytes(V.tensor_to_desc(d_glob)["l3_len"], world)[rank]
+        del d_glob
+        n_gen, first = hi - lo, lo
     else:
         n_gen, first = n_cfg, rank * n_cfg
     # batches of the rotation, carved from one allocation (each batch its own arena view)
-    nb = 1 if (nat or n_gen * stride >= ROTATE_BYTES) else min(64, -(-ROTATE_BYTES // (n_gen * stride)))
-    arena_all = torch.zeros(nb * n_gen * stride, dtype=torch.uint8, device="cuda")
+    nb = 1 if (nat or n_gen * stride >= ROTATE_BYTES or n_gen == 0) else min(64, -(-ROTATE_BYTES // (n_gen * stride)))
+    arena_all = torch.zeros(max(nb * n_gen * stride, 16), dtype=torch.uint8, device="cuda")
     arenas = [arena_all[b * n_gen * stride:(b + 1) * n_gen * stride] for b in range(nb)]
-    d_alls = [torch.zeros(n_gen * 16, dtype=torch.uint8, device="cuda") for _ in range(nb)]
+    d_alls = [torch.zeros(max(n_gen, 1) * 16, dtype=torch.uint8, device="cuda") for _ in range(nb)]
     for b in range(nb):   # batch b > 0: a disjoint sub-stream after every rank's batch 0
         V.synth(arenas[b], n_gen, stride, 0, synth_id, SEED, first + b * world * n_cfg, d_alls[b], stream=stream)
     torch.cuda.synchronize()
-    arena, d_all = arenas[0], d_alls[0]
-    desc_all = V.tensor_to_desc(d_all)
-    if strong:
-        lo, hi = shard_by_bytes(desc_all["l3_len"], world)[rank]
-    else:
-        lo, hi = 0, n_gen
-    n = hi - lo
-    d = d_all[lo * 16:hi * 16]
-    desc_np = desc_all[lo:hi]
+    arena, d = arenas[0], d_alls[0]
+    n = n_gen
+    desc_np = V.tensor_to_desc(d)[:n]
     out = torch.zeros(max(n, 1), dtype=torch.int32, device="cuda")
     status = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
 
     if nat:
         # valid input checksums, then a per-packet rewrite of src/dst IP and ports (seeded table,
         # regenerable on the host for the gate)
-        V.compute(arena, d_all, n_gen, None, None, V.MODE_WRITE, stream=stream)
-        rw_np = np.zeros(n_gen, V.NAT4_DTYPE)
+        V.compute(arena, d, n, None, None, V.MODE_WRITE, stream=stream)
+        rw_np = np.zeros(n_cfg, V.NAT4_DTYPE)   # the global table; this rank's entries [first, +n)
         g = np.random.default_rng(SEED)
-        rw_np.view(np.uint8).reshape(-1, 16)[:, :12] = g.integers(0, 256, (n_gen, 12), dtype=np.uint8)
+        rw_np.view(np.uint8).reshape(-1, 16)[:, :12] = g.integers(0, 256, (n_cfg, 12), dtype=np.uint8)
         rw_np["mask"] = V.NAT_SRC | V.NAT_DST | V.NAT_SPORT | V.NAT_DPORT
-        rw = torch.from_numpy(rw_np.view(np.uint8)).cuda()[lo * 16:hi * 16]
+        rw_np = np.ascontiguousarray(rw_np[first:first + n])
+        rw = torch.from_numpy(rw_np.view(np.uint8).copy()).cuda()
         bytes_per_step = n * NAT_BYTES_PER_PKT
 
         def step(i=0):
             V.nat4(arena, d, rw, n, None, V.NAT_RFC1624, stream=stream)
     else:
         bytes_per_step = algorithmic_bytes(desc_np)
-        ds = [dd[lo * 16:hi * 16] for dd in d_alls]
-        batch_bytes = [bytes_per_step] + [algorithmic_bytes(V.tensor_to_desc(dd)[lo:hi]) for dd in d_alls[1:]]
+        ds = d_alls
+        batch_bytes = [bytes_per_step] + [algorithmic_bytes(V.tensor_to_desc(dd)[:n]) for dd in d_alls[1:]]
 
         def step(i=0):
             # one pass over batch i mod nb: every IP header + L4 checksum -> out (4 B/packet)
@@ -356,7 +372,8 @@ def main():
     dev_id = str(getattr(props, "uuid", "")) or f"{props.pci_domain_id}:{props.pci_bus_id}:{props.pci_device_id}"
     ranks_info = gather_over_ranks({"rank": rank, "device": torch.cuda.current_device(), "device_id": dev_id,
                                     "kernel_ms": round(t_beg.elapsed_ms(t_end) / args.steps, 5),
-                                    "packets": int(n)})
+                                    "packets": int(n), "first_packet": int(first),
+                                    "peak_alloc_bytes": int(torch.cuda.max_memory_allocated())})
     # bytes of the K timed launches (the rotation's batches differ slightly in C3's mix)
     timed_bytes = sum(batch_bytes[i % nb] for i in range(args.steps)) if not nat else bytes_per_step * args.steps
     total_bytes_step = sum_over_ranks(float(timed_bytes)) / args.steps
@@ -367,33 +384,43 @@ def main():
     # measured read ceilings (context for the roofline fraction)
     sink = torch.zeros(8192, dtype=torch.int32, device="cuda")
     e0, e1 = V.Event(), V.Event()
-    read_ceiling = pattern_ceiling = unit_order_ceiling = launch_read = None
+    read_ceiling = read_bpc = pattern_ceiling = unit_order_ceiling = launch_read = None
     if not nat and n:
+        # a reference, not a ceiling: a contiguous streaming read of the whole rotation's arena
+        # (every byte, where K2 reads 1504 of every 2048), best of four grids
         span = arena_all[int(desc_np["l3_off"].min()) // 16 * 16:]   # every batch of the rotation
-        for _ in range(3):
-            V.read_probe(span, span.numel(), sink, stream=stream)
-        e0.record(stream)
-        for _ in range(10):
-            V.read_probe(span, span.numel(), sink, stream=stream)
-        e1.record(stream)
-        read_ceiling = span.numel() / (e0.elapsed_ms(e1) / 10 * 1e-3) / 1e9
+        cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+        best = None
+        for bpc in (2, 4, 8, 16):
+            for _ in range(3):
+                V.read_probe(span, span.numel(), sink, cus * bpc, stream=stream)
+            e0.record(stream)
+            for _ in range(10):
+                V.read_probe(span, span.numel(), sink, cus * bpc, stream=stream)
+            e1.record(stream)
+            r = span.numel() / (e0.elapsed_ms(e1) / 10 * 1e-3) / 1e9
+            if best is None or r > best[0]:
+                best = (r, bpc)
+        read_ceiling, read_bpc = best
         if desc_np["l3_len"].mean() >= 512 and arena.numel() < (1 << 32):
             # a read-only kernel over exactly this batch's chunks (no checksum work), best of 2
-            # and 4 workgroups per CU, in algorithmic bytes like `achieved`
-            cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+            # and 4 workgroups per CU, plain and with software-pipelined trips (bit 30), in
+            # algorithmic bytes like `achieved`
             pms = []
             for bpc in (2, 4):
-                for _ in range(3):
-                    V.pattern_probe(arena, d, n, sink, cus * bpc, stream=stream)
-                e0.record(stream)
-                for _ in range(10):
-                    V.pattern_probe(arena, d, n, sink, cus * bpc, stream=stream)
-                e1.record(stream)
-                pms.append(e0.elapsed_ms(e1) / 10)
+                for pipe in (0, 1 << 30):
+                    for _ in range(3):
+                        V.pattern_probe(arena, d, n, sink, (cus * bpc) | pipe, stream=stream)
+                    e0.record(stream)
+                    for _ in range(10):
+                        V.pattern_probe(arena, d, n, sink, (cus * bpc) | pipe, stream=stream)
+                    e1.record(stream)
+                    pms.append(e0.elapsed_ms(e1) / 10)
             pattern_ceiling = bytes_per_step / (min(pms) * 1e-3) / 1e9
             # the same reads in K2's packet order (a wave walks its own 64 consecutive packets,
-            # grid-strided units): the order costs C3 ~9% against the grid order above (DESIGN.md
-            # §5 item 24), so the kernel is also reported against this one
+            # grid-strided units): a reference order, not a ceiling (K2 beats it on C2 through its
+            # rotated slot order; on C3 the order costs ~9% against the grid
+            # order above, item 24)
             pus = []
             for bpc in (5, 12):
                 for _ in range(3):
@@ -442,19 +469,22 @@ def main():
 
     # correctness: (1) rank 0 against the oracle on the cpu_baseline's packets (2) every rank:
     # sums written in place, then verified on the GPU
+    # every line carries the CPU baseline, N > 1 included: rank 0 times it after the timed region
+    # (the other ranks wait at the next collective), on rank 0's first packets
     cpu, gate = None, {}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not nat:
-        cpu, (m, want_out, want_st) = cpu_baseline(args.workload, synth_id, stride, first + lo, args.cpu_budget)
+    if rank == 0 and not args.no_cpu_baseline and not nat and n:
+        cpu, (m, want_out, want_st) = cpu_baseline(args.workload, synth_id, stride, first, args.cpu_budget)
+        m = min(m, n)
         got = out[:m].cpu().numpy().view(np.uint32)
         gate["oracle_packets"] = int(m)
-        gate["oracle_equal"] = bool(np.array_equal(got, want_out))
-    elif rank == 0 and world == 1 and not args.no_cpu_baseline and nat:
-        cpu, (m, a0, d0, want) = cpu_baseline_nat(np.ascontiguousarray(rw_np[lo:hi]), args.cpu_budget)
+        gate["oracle_equal"] = bool(np.array_equal(got, want_out[:m]))
+    elif rank == 0 and not args.no_cpu_baseline and nat and n:
+        cpu, (m, a0, d0, want) = cpu_baseline_nat(rw_np, args.cpu_budget)   # rank 0: first == 0
         got = arena[:m * stride].cpu().numpy()
         gate["oracle_packets"] = int(m)
         gate["oracle_equal"] = bool(np.array_equal(got, want))
     if not nat and n:
-        gate.update(oracle_sample_gate(synth_id, stride, first + lo, out[:n].cpu().numpy().view(np.uint32)))
+        gate.update(oracle_sample_gate(synth_id, stride, first, out[:n].cpu().numpy().view(np.uint32)))
     if nat:
         ok = True
         if n:
@@ -478,6 +508,7 @@ def main():
     achieved = timed_bytes / args.steps / (kernel_ms * 1e-3) / 1e9 if n else 0.0
     # C5's summary: the 10M-packet pass with the bench's rewrite mask (src|dst|ports = 15)
     traffic, traffic_src = pmc_traffic("nat15" if nat else args.workload, n) if args.team == 0 else (None, None)
+    traffic_src = traffic_src or {}
     if rank == 0:
         value = total_bytes_step * args.steps / wall_max / 1e9
         kname = "k_natq (RFC 1624)" if nat else "k_csum_d (K2)"
@@ -496,7 +527,8 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": desc_text + (" (one global batch, byte-balanced shards)" if strong else " per GPU"),
-                "global_batch": n_gen if strong else n_gen * world,
+                "global_batch": n_cfg if strong else n_cfg * world,
+                "source_hash": source_hash(),
                 "packets_rank0": n,
                 "algorithmic_bytes_per_step_rank0": bytes_per_step,
                 "algorithmic_bytes_per_step_all_ranks": int(total_bytes_step),
@@ -522,14 +554,20 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
                 "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, corrected)",
-                "traffic_source": traffic_src,
+                "traffic_source": traffic_src.get("source"),
+                # the tree the PMC summary was measured on; stale: no summary of this tree's sources
+                "traffic_head": traffic_src.get("head"),
+                "traffic_stale": traffic_src.get("stale"),
                 "algorithmic_bytes_per_launch": bytes_per_step,
                 "kernel_avg_ms": round(kernel_ms, 5),
-                "measured_read_ceiling_GBps": round(read_ceiling, 1) if read_ceiling else None,
+                # references (not bounds): a contiguous read of the whole span, and K2's reads in
+                # its own unit order without the rotation
+                "contiguous_read_GBps": round(read_ceiling, 1) if read_ceiling else None,
+                "contiguous_read_workgroups_per_cu": read_bpc,
                 "measured_pattern_ceiling_GBps": round(pattern_ceiling, 1) if pattern_ceiling else None,
                 "frac_of_pattern_ceiling": round(achieved / pattern_ceiling, 4) if pattern_ceiling else None,
-                "measured_unit_order_ceiling_GBps": round(unit_order_ceiling, 1) if unit_order_ceiling else None,
-                "frac_of_unit_order_ceiling": round(achieved / unit_order_ceiling, 4) if unit_order_ceiling else None,
+                "reference_order_probe_GBps": round(unit_order_ceiling, 1) if unit_order_ceiling else None,
+                "frac_of_reference_order_probe": round(achieved / unit_order_ceiling, 4) if unit_order_ceiling else None,
                 "pattern_ceiling_kernel": ("k_natq probe (same loads and stores, no rewrite)" if nat else
                                            "k_pattern_probe (K2's chunk reads, no checksum work)")
                 if pattern_ceiling else None,

@@ -212,7 +212,9 @@ int vpcsum_nat4_pattern_probe_async(uint8_t* d_arena, uint64_t arena_len, const 
                                     const vpcsum_nat4_t* d_rw, uint32_t n, void* stream);
 
 /* Synthetic workload generator (bench / tests): deterministic counter-based splitmix64 bytes,
- * identical to oracle/csum_oracle.c:orc_synth_frame.  workload: see VPCSUM_SYNTH_*. */
+ * identical to oracle/csum_oracle.c:orc_synth_frame.  workload: see VPCSUM_SYNTH_*.  d_arena NULL
+ * (with d_desc set): the descriptors alone, e.g. the lengths a rank needs to cut one global batch
+ * into byte-balanced shards before it generates only its own. */
 #define VPCSUM_SYNTH_C1_UDP64     1  /* IPv4/UDP L3 50 B                     */
 #define VPCSUM_SYNTH_C2_TCP1500   2  /* IPv4/TCP L3 1500 B                   */
 #define VPCSUM_SYNTH_C3_MIXED     3  /* IPv4 {64,576,1500} x {UDP,TCP,ICMP}  */

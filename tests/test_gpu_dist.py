@@ -63,6 +63,47 @@ def test_bench_two_ranks_strong(workload):
         < 0.01 * c["algorithmic_bytes_per_step_all_ranks"]
 
 
+def test_bench_two_ranks_strong_shards_per_rank_with_cpu_baseline():
+    """Strong C4 over two ranks: each rank generates and holds only its own byte-balanced slice of
+    the global batch (rank 1 starts where rank 0 ends; a rank's peak allocation is about half the
+    global arena, not all of it), and the N > 1 line carries the CPU baseline (VERIFY r3 item 2)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--ramp-ms", "0", "--share-gpu", "--workload", "c4", "--strong", "--cpu-budget", "0.3"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    j = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    c = j["config"]
+    r0, r1 = c["ranks"]
+    assert r0["first_packet"] == 0 and r1["first_packet"] == r0["packets"]
+    assert r0["packets"] + r1["packets"] == c["global_batch"] == 1 << 18
+    global_arena = (1 << 18) * 9216
+    for rr in (r0, r1):
+        assert rr["peak_alloc_bytes"] < 0.6 * global_arena, rr
+    assert j["cpu_baseline"] and j["cpu_baseline"]["value"] > 0 and j["cpu_baseline"]["cores"] >= 1
+    assert c["oracle_gate"]["oracle_equal"] is True and c["oracle_gate"]["sample_equal"] is True
+
+
+def test_descriptor_only_synth_equals_full_synth():
+    """vpcsum_synth_async with a NULL arena writes the same descriptors as the full generator (the
+    lengths a strong rank cuts the global batch with)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vproxy_amd import vpcsum as V
+    for wl, stride in ((V.SYNTH_C3, 2048), (V.SYNTH_FUZZ, 9216), (V.SYNTH_C4, 9216)):
+        n = 5000
+        arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+        d1 = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+        d2 = torch.full((n * 16,), 0x5a, dtype=torch.uint8, device="cuda")
+        V.synth(arena, n, stride, 14, wl, 99, 12345, d1)
+        V.synth(None, n, stride, 14, wl, 99, 12345, d2)
+        torch.cuda.synchronize()
+        assert torch.equal(d1, d2), wl
+
+
 def test_bench_refuses_more_ranks_than_gpus():
     """Without --share-gpu, more ranks than visible cards is an error (no "N-GPU" line from ranks
     sharing one card)."""

@@ -1,0 +1,77 @@
+#!/bin/bash
+# Round-4 measurement call: GPU tests, bench lines of every config, kernel trace of the headline,
+# PMC passes (C2, C1, C3, NAT full / read-only / pattern probe), host path.  Every GPU step has its own time limit; a
+# crash / abort / timeout (exit > 1) ends the script.  usage: tools/gpu_r04.sh <tag> [parts]
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${1:-r04}; PARTS=${2:-tests,bench,trace,pmc,host}
+step() {  # name, limit, cmd...
+  local name=$1 lim=$2; shift 2
+  echo "=== $name $(date +%T)"
+  timeout -k 10 "$lim" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1
+  local rc=$?
+  echo "rc($name)=$rc"; tail -n 2 "gpurun_out/${TAG}_$name.log"
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+has() { [[ ",$PARTS," == *",$1,"* ]]; }
+# the measured tree: the hash of the library sources on this box (tools/save_profiles.py stores it
+# in every summary.json; bench.py matches PMC summaries against it)
+python -c "import json; from vproxy_amd.build import source_hash; print(json.dumps({'src_hash': source_hash()}))" > gpurun_out/${TAG}_src.json || exit 1
+if has tests; then
+  step gputest 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+fi
+if has smoke; then
+  step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if has benchc2; then
+  step bench_c2 300 python bench.py --steps 200 --warmup 20
+  step bench_c5 400 python bench.py --workload c5 --steps 50 --warmup 5
+fi
+if has bench; then
+  step bench_c2 300 python bench.py --steps 200 --warmup 20
+  for w in c1 c3 c4; do step bench_$w 300 python bench.py --workload $w --steps 200 --warmup 20; done
+  step bench_c4_strong 300 python bench.py --workload c4 --strong --steps 200 --warmup 20 --no-cpu-baseline
+  step bench_c5 400 python bench.py --workload c5 --steps 50 --warmup 5
+fi
+if has trace; then
+  step trace_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline
+fi
+if has pmc || has pmck2; then   # pmck2: the checksum configs only (PMC_CFGS, default all four)
+  # FETCH_SIZE takes 3 of the 4 TCC counters and WRITE_SIZE 2: never in one pass
+  P="FETCH_SIZE|WRITE_SIZE|SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES|SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES|GRBM_GUI_ACTIVE TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"
+  for w in ${PMC_CFGS:-c2 c1 c3 c4}; do
+    IFS='|' read -ra PS <<< "$P"; i=0
+    for c in "${PS[@]}"; do i=$((i+1)); step pmc_${w}_p$i 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_$w -o p$i -- python3 tools/prof_one.py --workload $w; done
+  done
+fi
+if has pmc || has pmcnat; then
+  N="FETCH_SIZE|WRITE_SIZE|TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum|SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES"
+  for m in ${NAT_MASKS:-15 0}; do
+    IFS='|' read -ra PS <<< "$N"; i=0
+    for c in "${PS[@]}"; do i=$((i+1)); step pmc_nat${m}_p$i 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_nat$m -o p$i -- python3 tools/prof_one.py --nat 0 --nat-mask $m; done
+  done
+fi
+if has pmc || has pmcnat || has pmcnatprobe; then   # NAT's memory operations without the rewrite
+  N="FETCH_SIZE|WRITE_SIZE|TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum"
+  IFS='|' read -ra PS <<< "$N"; i=0
+  for c in "${PS[@]}"; do i=$((i+1)); step pmc_natprobe_p$i 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_natprobe -o p$i -- python3 tools/prof_one.py --nat 0 --nat-mask 15 --nat-probe; done
+  step trace_natprobe 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace_nat -o run -- python3 tools/prof_one.py --nat 0 --nat-mask 15 --nat-probe --iters 20
+fi
+if has pmc32; then   # last: a counter this gfx950 image may not have
+  step pmc_nat15_p32 120 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/${TAG}_pmc_nat15 -o p32 -- python3 tools/prof_one.py --nat 0 --nat-mask 15
+fi
+if has host; then
+  step hostpath 400 python tools/hostpath.py
+fi
+if has flush; then   # tools/flush_latency is built in-tree beforehand (g++ line in its header)
+  step flush 300 ./tools/flush_latency 2000
+fi
+if has rank8; then   # 8 ranks on one card: the strong shards per rank, a functional rehearsal
+  step bench_c4s_8rank 600 python bench.py --workload c4 --strong --gpus 8 --steps 50 --warmup 5 --share-gpu --ramp-ms 300
+  step bench_c5_8rank 600 python bench.py --workload c5 --gpus 8 --steps 20 --warmup 3 --share-gpu --ramp-ms 300
+fi
+if has rank2; then   # the multi-rank path rehearsed on one GPU (bench.py launches its own ranks)
+  step bench_c2_2rank 300 python bench.py --gpus 2 --steps 50 --warmup 5 --no-cpu-baseline --share-gpu
+  step bench_c5_2rank 400 python bench.py --workload c5 --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline --share-gpu
+fi
+echo ALLDONE

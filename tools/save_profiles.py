@@ -6,18 +6,47 @@ profiles/ (tooling).  Usage: python tools/save_profiles.py <tag>
   <tag>_pmc_<cfg>/pass<i>.csv     --pmc passes, rows of the measured kernel only
   <tag>_pmc_<cfg>/summary.json    per-launch means + HBM bytes (tools/traffic.py rules)
   <tag>_hostpath_c2.json          tools/hostpath.py
+
+Every summary.json records the tree it measured: `src_hash` (vproxy_amd/build.py:source_hash of the
+library sources, computed on the GPU box into gpurun_out/<tag>_src.json by the measurement script),
+`head` / `head_time` (this repo's HEAD when the summary was saved; `head_matches_src` says whether
+HEAD's sources hash to `src_hash`), so bench.py can take the traffic of the tree it benches.
 """
 import csv
 import glob
 import json
 import os
 import shutil
+import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 G = os.path.join(REPO, "gpurun_out")
 P = os.path.join(REPO, "profiles")
 PACKETS = {"c1": 1 << 20, "c2": 1 << 20, "c3": 1 << 20, "c4": 1 << 18}
+sys.path.insert(0, REPO)
+from vproxy_amd.build import source_hash  # noqa: E402
+
+
+def git(*args) -> str:
+    return subprocess.check_output(["git", "-C", REPO] + list(args), text=True).strip()
+
+
+def provenance(tag: str) -> dict:
+    """The measured tree (the box's source hash, else this tree's) and this repo's HEAD."""
+    f = os.path.join(G, f"{tag}_src.json")
+    src = json.load(open(f))["src_hash"] if os.path.exists(f) else source_hash()
+    head = git("rev-parse", "HEAD")
+    head_src = source_hash(lambda p: _show(head, p))
+    return {"tag": tag, "src_hash": src, "head": head, "head_time": int(git("show", "-s", "--format=%ct", head)),
+            "head_matches_src": head_src == src and source_hash() == src}
+
+
+def _show(commit: str, path: str):
+    try:
+        return subprocess.check_output(["git", "-C", REPO, "show", f"{commit}:{path}"], stderr=subprocess.DEVNULL)
+    except subprocess.CalledProcessError:
+        return None
 
 
 def json_line(log):
@@ -29,7 +58,7 @@ def json_line(log):
     return None
 
 
-def summarise(src, dst, kern, packets):
+def summarise(src, dst, kern, packets, prov=None):
     """Mean of each counter over the kernel's dispatches, plus HBM bytes per launch.  Reads:
     FETCH_SIZE = TCC_EA0_RDREQ x 64 B, and every read request of these kernels is 128 B
     (TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ for K2 on C1-C3 and for the NAT kernel's scattered header
@@ -48,7 +77,8 @@ def summarise(src, dst, kern, packets):
         for r in keep:
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     mean = {k: sum(v) / len(v) for k, v in vals.items()}
-    out = {"kernel_substring": kern, "packets": packets, "dispatches": len(vals.get("FETCH_SIZE", [])), **mean}
+    out = {"kernel_substring": kern, "packets": packets, "dispatches": len(vals.get("FETCH_SIZE", [])),
+           **(prov or {}), **mean}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         rd, wr = mean["FETCH_SIZE"] * 1024, mean["WRITE_SIZE"] * 1024
         out["write_bytes"] = wr
@@ -73,12 +103,15 @@ def resummarise(tag):
         os.makedirs(tmp, exist_ok=True)
         for f in glob.glob(os.path.join(dst, "pass*.csv")):
             shutil.copy(f, os.path.join(tmp, "p" + os.path.basename(f)[4:-4] + "_counter_collection.csv"))
-        summarise(tmp, dst, old["kernel_substring"], old["packets"])
+        summarise(tmp, dst, old["kernel_substring"], old["packets"],
+                  {k: old[k] for k in ("tag", "src_hash", "head", "head_time", "head_matches_src", "provenance")
+                   if k in old})
         shutil.rmtree(tmp)
 
 
 def main(tag):
     os.makedirs(P, exist_ok=True)
+    prov = provenance(tag)
     for cfg in ("c2", "c1", "c3", "c4", "c4_strong", "c5"):
         d = json_line(os.path.join(G, f"{tag}_bench_{cfg}.log"))
         if d:
@@ -92,7 +125,7 @@ def main(tag):
         cfg = os.path.basename(src)[len(tag) + 5:]
         nat = cfg.startswith("nat")
         summarise(src, os.path.join(P, f"{tag}_pmc_{cfg}"), "vpcsum::k_nat" if nat else "k_csum",
-                  10_000_000 if nat else PACKETS[cfg])
+                  10_000_000 if nat else PACKETS[cfg], prov)
     d = json_line(os.path.join(G, f"{tag}_hostpath.log"))
     if d:
         json.dump(d, open(os.path.join(P, f"{tag}_hostpath_c2.json"), "w"), indent=1)

@@ -22,6 +22,29 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def source_files() -> list[str]:
+    """Repo-relative paths of every file the library is built from."""
+    return sorted(os.path.relpath(os.path.normpath(os.path.join(CSRC, s)), REPO) for s in SOURCES + HEADERS)
+
+
+def source_hash(read=None) -> str:
+    """Hash of the library's sources (the evidence key of profiles/*/summary.json: a PMC summary
+    describes the kernels of exactly one source tree).  read(path) -> bytes | None lets tooling
+    hash the tree of a past commit; the default reads the working tree."""
+    import hashlib
+    if read is None:
+        def read(p):
+            f = os.path.join(REPO, p)
+            return open(f, "rb").read() if os.path.exists(f) else None
+    h = hashlib.sha256()
+    for p in source_files():
+        b = read(p)
+        if b is None:
+            continue
+        h.update(p.encode() + b"\0" + str(len(b)).encode() + b"\0" + b)
+    return h.hexdigest()[:16]
+
+
 def _stale() -> bool:
     if not os.path.exists(LIB):
         return True

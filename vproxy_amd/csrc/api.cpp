@@ -317,12 +317,12 @@ int vpcsum_pattern_probe_async(const uint8_t* d_arena, uint64_t arena_len, const
 int vpcsum_synth_async(uint8_t* d_arena, uint64_t arena_len, uint32_t n, uint32_t stride, uint32_t l3_pad,
                        uint32_t workload, uint64_t seed, uint64_t first_index, vpcsum_desc_t* d_desc, void* stream) {
     if (n == 0) return 0;
-    if (!d_arena) return fail("vpcsum_synth_async: NULL arena");
+    if (!d_arena && !d_desc) return fail("vpcsum_synth_async: NULL arena and descriptors");
     if (workload < VPCSUM_SYNTH_C1_UDP64 || workload > VPCSUM_SYNTH_C5_NAT1500) return fail("vpcsum_synth_async: bad workload %u", workload);
     const uint32_t maxlen = (workload == VPCSUM_SYNTH_C4_V6JUMBO || workload == VPCSUM_SYNTH_FUZZ) ? 9000
                             : (workload == VPCSUM_SYNTH_C1_UDP64) ? 50 : 1500;
     if ((uint64_t)l3_pad + maxlen > stride) return fail("vpcsum_synth_async: stride %u < l3_pad %u + %u", stride, l3_pad, maxlen);
-    if ((uint64_t)n * stride > arena_len) return fail("vpcsum_synth_async: arena too small");
+    if (d_arena && (uint64_t)n * stride > arena_len) return fail("vpcsum_synth_async: arena too small");
     VPC_CHECK(launch_synth(d_arena, arena_len, n, stride, l3_pad, workload, seed, first_index, d_desc,
                            (hipStream_t)stream),
               "synth launch");

@@ -1811,10 +1811,26 @@ __device__ Shape shape_of(uint32_t workload, uint64_t seed, uint64_t pkt) {
 }
 
 // One block per packet: threads fill the payload 8 bytes at a time, then thread 0 writes
-// the header fields (same order as the oracle: payload first, headers overwrite).
+// the header fields (same order as the oracle: payload first, headers overwrite).  arena NULL:
+// the descriptors alone.
 __global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ arena, uint32_t n, uint32_t stride,
                                               uint32_t l3_pad, uint32_t workload, uint64_t seed,
                                               uint64_t first, vpcsum_desc_t* __restrict__ desc) {
+    if (!arena) {   // descriptors only: one lane per packet
+        for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+            const Shape s = shape_of(workload, seed, first + p);
+            vpcsum_desc_t d;
+            d.l3_off = (uint64_t)p * stride + l3_pad;
+            d.l3_len = (uint16_t)s.l3_len;
+            d.l4_off = (uint16_t)s.l4_off;
+            d.l3_ver = (uint8_t)s.ver;
+            d.l4_proto = (uint8_t)s.proto;
+            d.flags = (uint8_t)((s.ver == 4 ? VPCSUM_F_IP : 0) | VPCSUM_F_L4);
+            d.rsv = 0;
+            desc[p] = d;
+        }
+        return;
+    }
     for (uint32_t p = blockIdx.x; p < n; p += gridDim.x) {
         const uint64_t pkt = first + p;
         const Shape s = shape_of(workload, seed, pkt);

@@ -230,8 +230,10 @@ def read_probe(buf, nbytes: int, sink, grid: int = 0, stream=None):
 
 def synth(arena, n: int, stride: int, l3_pad: int, workload: int, seed: int, first_index: int = 0,
           desc=None, stream=None):
-    _check(lib().vpcsum_synth_async(_ptr(arena), arena.numel(), n, stride, l3_pad, workload, seed, first_index,
-                                    _ptr(desc), _stream(stream)), "vpcsum_synth_async")
+    """arena None: the descriptors alone (desc required)."""
+    _check(lib().vpcsum_synth_async(_ptr(arena) if arena is not None else None, arena.numel() if arena is not None else 0,
+                                    n, stride, l3_pad, workload, seed, first_index, _ptr(desc), _stream(stream)),
+           "vpcsum_synth_async")
 
 
 class Event:
