@@ -59,10 +59,10 @@ def test_k2_default_builds_budgets():
     unstaged_compute = pick(ks, r"k_csum_dILi8ELi6ELi2ELi2ELb0ELb[01]ELi1ELi0ELin9ELb1ELb0ELb0E")
     staged_compute = pick(ks, r"k_csum_dILi8ELi6ELi2ELi2ELb0ELb[01]ELi1ELi0ELin9ELb1ELb0ELb1E")
     verify = pick(ks, r"k_csum_dILi8ELi6ELi2ELi2ELb1ELb[01]ELi1ELi0ELin9ELb1ELb0ELb[01]E")
-    for k, v in unstaged_compute.items():
-        assert v["vgpr_count"] <= 80, (k, v)        # 6 waves per SIMD
-    for k, v in {**staged_compute, **verify}.items():
-        assert v["vgpr_count"] <= 96, (k, v)        # 5 waves per SIMD
+    # every default build fits 6 waves per SIMD (the verify and staging builds since round 4:
+    # stored fields loaded in phase A, a scalar wave index, opaque result-store indices)
+    for k, v in {**unstaged_compute, **staged_compute, **verify}.items():
+        assert v["vgpr_count"] <= 80, (k, v)
     for k, v in {**unstaged_compute, **staged_compute, **verify}.items():
         assert v["private_segment_fixed_size"] == 0, (k, v)
     # the slot plans, and the staged result words: 16 KiB and 26 KiB per workgroup

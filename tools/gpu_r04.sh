@@ -70,6 +70,9 @@ if has rank8; then   # 8 ranks on one card: the strong shards per rank, a functi
   step bench_c4s_8rank 600 python bench.py --workload c4 --strong --gpus 8 --steps 50 --warmup 5 --share-gpu --ramp-ms 300
   step bench_c5_8rank 600 python bench.py --workload c5 --gpus 8 --steps 20 --warmup 3 --share-gpu --ramp-ms 300
 fi
+if has ab; then   # this tree's library against vproxy_amd/libvpcsum_ab.so, uncached batches, compute + verify
+  step ab 1100 bash tools/ab_libs_cold.sh ${TAG}_ab "${AB_WS:-c1 c3 c2}" ${AB_ROUNDS:-2} "${AB_MODES:-0 1}"
+fi
 if has rank2; then   # the multi-rank path rehearsed on one GPU (bench.py launches its own ranks)
   step bench_c2_2rank 300 python bench.py --gpus 2 --steps 50 --warmup 5 --no-cpu-baseline --share-gpu
   step bench_c5_2rank 400 python bench.py --workload c5 --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline --share-gpu

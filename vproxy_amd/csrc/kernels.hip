@@ -393,11 +393,12 @@ __device__ __forceinline__ void wave_sync_lds() {
 __device__ __forceinline__ uint32_t hsum(uint32_t acc, uint32_t w) { return __builtin_amdgcn_sad_u16(w, 0u, acc); }
 
 // Fast-class trips of one team over its packet's chunks [0, nch): U loads per lane issued
-// back to back, then consumed (payload fast path, masked tail, header bitmaps).
-template <int TEAM, int U, bool VERIFY, bool NT>
+// back to back, then consumed (payload fast path, masked tail, header bitmaps).  The stored
+// checksum fields (verify) are not summed here: the owner lane loads them in phase A.
+template <int TEAM, int U, bool NT>
 __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, uint32_t boff, int nch, int klo,
                                            uint32_t kfast, int l4hi, const uint4 bm, int tl, uint32_t& acc_l4,
-                                           uint32_t& acc_ip, uint32_t& st_ip, uint32_t& st_l4) {
+                                           uint32_t& acc_ip) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     for (int rr = 0; rr * TEAM < nch; rr += U) {
         v4u v[U];
@@ -425,10 +426,6 @@ __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, ui
                     const int hb = hb0 + 2 * j;
                     acc_ip = hsum(acc_ip, w[j] & hmask((bm.x >> hb) & 3));
                     acc_l4 = hsum(acc_l4, w[j] & hmask((bm.y >> hb) & 3));
-                    if (VERIFY) {
-                        st_ip += w[j] & hmask((bm.z >> hb) & 3);
-                        st_l4 += w[j] & hmask((bm.w >> hb) & 3);
-                    }
                 }
             }
             asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
@@ -455,7 +452,7 @@ __device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uin
     uint32_t h_l4 = 0, h_ip = 0;   // fast class: halfword sums
     if (a.y >> 31) {
         const uint4 bm = sl[1];
-        fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip, st_ip, st_l4);
+        fast_trips<TEAM, U, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip);
     } else if (nch > 0) {
         const uint4 q2 = sl[2], q3 = sl[3];
         PktPlan pl;
@@ -617,6 +614,22 @@ __device__ __forceinline__ uint4 win_sums(const uint32_t (&x)[20], int sh, int v
     return make_uint4(fold32(l4), fold32(ip), 0u, VERIFY ? (st_l4 | (st_ip << 16)) : 0u);
 }
 
+// One packet's result word and status byte, stored where the unit's owner lanes store them.  The
+// index goes through an opaque copy: hoisted, `out + lane` would be a 64-bit per-lane address kept
+// live (or spilled) across the whole unit loop for a store issued once per unit.
+template <bool NT>
+__device__ __forceinline__ void store_result(uint32_t* out, uint8_t* status, uint32_t idx, uint32_t res_out,
+                                             uint32_t res_st) {
+    asm volatile("" : "+v"(idx));
+    if (NT) {
+        if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + idx));
+        if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + idx));
+    } else {
+        if (out) out[idx] = res_out;
+        if (status) status[idx] = (uint8_t)res_st;
+    }
+}
+
 // K2 body for workgroup `blk` of a grid of `gdim` workgroups (k_csum_d: the launch grid;
 // k_csum_service: the persistent service grid, once per batch).
 // ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
@@ -633,7 +646,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
     const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: an SGPR
     // packet of this lane = P0 + lo.  IL = 0: a wave owns 64 consecutive packets.  IL = 1: the 4
     // waves of a workgroup interleave in groups of 8 over 256 consecutive packets, so the teams
     // of the whole workgroup read one contiguous 64-KB window per iteration (one DRAM stream
@@ -726,6 +739,8 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         int fld = -1;
         int key = 0;
         int n_small = 0, n_cls = 0;   // n_cls: distinct cost classes in the large tier
+        bool fastc = false;           // fast class (header bitmaps; L3 and L4 at even offsets)
+        uint32_t ld_sip = 0, ld_sl4 = 0;   // verify, fast class: the stored fields, loaded in phase A
         bool fastu = false;           // window unit (SF): sums in fsums, no slots
         uint4 fsums = make_uint4(0, 0, 0, 0);
         // Window units (SF): the 64 packets of the unit have one shape (descriptor fields, flags
@@ -848,12 +863,8 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                         if (DS && stage) {
                             s_eo[wid][es_n][lane] = res_out;
                             s_es[wid][es_n][lane] = (uint8_t)st;
-                        } else if (NT) {
-                            if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lo));
-                            if (status) __builtin_nontemporal_store((uint8_t)st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lo));
                         } else {
-                            if (out) out[P0 + lo] = res_out;
-                            if (status) status[P0 + lo] = (uint8_t)st;
+                            store_result<NT>(out, status, P0 + lo, res_out, st);
                         }
                     }
                 }
@@ -913,7 +924,19 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                     if (proto != 1) B_l4 |= (ver == 4) ? hw_range(r0h + 6, r0h + 10) : hw_range(r0h + 4, r0h + 20);
                 }
             }
-            const bool fastc = hbm && klo <= 4;
+            fastc = hbm && klo <= 4;
+            if (VERIFY) {
+                // The stored IP / L4 checksum fields of a fast-class packet (both at even
+                // addresses): two 2-B loads issued now and consumed in phase C, so their latency
+                // hides under phase B.  The teams then stream the packet without summing the fields
+                // through every trip and reducing them (two accumulators and two bitmaps live
+                // across the trip loop: the verify build held 95 VGPRs for it, 80 now).  The
+                // load's line is the one the packet's first chunk comes from (same policy: one
+                // fetch).  The slow class keeps its team sums of the fields.
+                const bool pre = !bad && fastc;
+                ld_sip = __builtin_amdgcn_raw_buffer_load_b16(rsrc, pre && do_ip ? (uint32_t)off + 10u : kOutOfRange, 0, NT ? 2 : 0);
+                ld_sl4 = __builtin_amdgcn_raw_buffer_load_b16(rsrc, pre && do_l4 ? (uint32_t)off + (uint32_t)(l4o + fld) : kOutOfRange, 0, NT ? 2 : 0);
+            }
             // cost class: bad first (key 0), then the small tier (one trip of TS x US chunks),
             // then trips of the large tier's team loop, the slow class last
             if (!bad) {
@@ -966,9 +989,10 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                             }
                         }
                         if (VERIFY) {
-                            if (do_ip && orient(sums.w >> 16, r0) == ipc) st |= VPCSUM_S_IP_OK;
+                            const uint32_t s_ip = fastc ? bswap16(ld_sip) : orient(sums.w >> 16, r0);
+                            if (do_ip && s_ip == ipc) st |= VPCSUM_S_IP_OK;
                             if (do_l4) {
-                                const uint32_t stored = orient(sums.w & 0xffff, r0 + l4o + fld);
+                                const uint32_t stored = fastc ? bswap16(ld_sl4) : orient(sums.w & 0xffff, r0 + l4o + fld);
                                 if (stored == l4c) st |= VPCSUM_S_L4_OK;
                                 if (!psonly && proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
                             }
@@ -987,13 +1011,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                 s_eo[wid][es_n][lane] = res_out;
                 s_es[wid][es_n][lane] = (uint8_t)res_st;
             } else if (live) {
-                if (NT) {
-                    if (out) __builtin_nontemporal_store(res_out, (__attribute__((address_space(1))) uint32_t*)(out + P0 + lo));
-                    if (status) __builtin_nontemporal_store((uint8_t)res_st, (__attribute__((address_space(1))) uint8_t*)(status + P0 + lo));
-                } else {
-                    if (out) out[P0 + lo] = res_out;
-                    if (status) status[P0 + lo] = (uint8_t)res_st;
-                }
+                store_result<NT>(out, status, P0 + lo, res_out, res_st);
             }
         };
 
@@ -1030,8 +1048,22 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     if (DS && stage) es_flush();
 }
 
+// Occupancy of a K2 build: WPE > 1 forces that many waves per SIMD (tuning variants).  The default
+// shape's verify and staging builds are held to 6 (80 VGPRs), the unstaged compute build's natural
+// count: left alone, the compiler gave them 95 and 92 (5 waves) -- the verify build for its stored
+// fields, the staging build because its 26 KB of LDS let it budget for fewer resident waves
+// (DESIGN.md §5 items 25, 28).  tests/test_kernel_resources.py holds all of them to 80, no scratch.
+template <int TEAM, int U, int TS, int US, bool VERIFY, int WPE, int IL, int ROT, bool SF, bool WT, bool DS>
+constexpr int k2_waves_per_eu() {
+    return WPE > 1 ? WPE
+                   : (TEAM == kDefaultTeam && U == kDefaultUnroll && TS == kSmallTeam && US == kSmallUnroll &&
+                      IL == 0 && ROT == kDefaultRot && SF && !WT && (VERIFY || DS))
+                         ? 6
+                         : 1;
+}
+
 template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_per_eu<TEAM, U, TS, US, VERIFY, WPE, IL, ROT, SF, WT, DS>()))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
