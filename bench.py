@@ -373,6 +373,7 @@ def main():
     ranks_info = gather_over_ranks({"rank": rank, "device": torch.cuda.current_device(), "device_id": dev_id,
                                     "kernel_ms": round(t_beg.elapsed_ms(t_end) / args.steps, 5),
                                     "packets": int(n), "first_packet": int(first),
+                                    "shard_arena_bytes": int(n) * stride,
                                     "peak_alloc_bytes": int(torch.cuda.max_memory_allocated())})
     # bytes of the K timed launches (the rotation's batches differ slightly in C3's mix)
     timed_bytes = sum(batch_bytes[i % nb] for i in range(args.steps)) if not nat else bytes_per_step * args.steps

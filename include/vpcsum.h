@@ -35,7 +35,9 @@
 extern "C" {
 #endif
 
-#define VPCSUM_ABI_VERSION 1
+/* 2 (round 4): VPCSUM_NAT_DEC_TTL refuses a TTL / hop limit <= 1 (S_BAD_DESC | S_TTL_EXPIRED)
+ * instead of writing 0; vpcsum_synth_async takes a NULL arena (descriptors only). */
+#define VPCSUM_ABI_VERSION 2
 
 /* ------------------------------------------------------------------------ */
 /* Data formats                                                             */

@@ -45,7 +45,7 @@ def test_so_loads_and_reports_abi(libpath):
     for f in header_functions():
         assert hasattr(L, f)
     L.vpcsum_abi_version.restype = ctypes.c_int
-    assert L.vpcsum_abi_version() == 1
+    assert L.vpcsum_abi_version() == 2
 
 
 def test_code_object_is_gfx950(libpath):
@@ -107,3 +107,15 @@ def test_survey_entry_points_refuse_before_init(libpath):
                                ctypes.c_uint32(0), ctypes.byref(h)) != 0
     assert L.vpcsum_register_arena(None, ctypes.c_uint64(0)) != 0
     assert L.vpcsum_shutdown() == 0   # nothing to shut down: a no-op
+
+
+def test_allocation_failure_returns_error(libpath, tmp_path):
+    """A host allocation failure inside an extern "C" entry returns -1 with a message instead of
+    unwinding a C++ exception into the caller (api.cpp VPC_CATCH): tests/cpp/alloc_fail.cpp makes
+    the global operator new throw during vpcsum_group_create_list (no GPU call before it)."""
+    exe = tmp_path / "alloc_fail"
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(REPO, "include"),
+                           os.path.join(REPO, "tests", "cpp", "alloc_fail.cpp"), "-L", os.path.dirname(libpath),
+                           "-lvpcsum", "-Wl,-rpath," + os.path.dirname(libpath), "-o", str(exe)])
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "out of host memory" in r.stdout, (r.returncode, r.stdout, r.stderr)

@@ -16,7 +16,9 @@
 #include <algorithm>
 #include <chrono>
 #include <map>
+#include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -25,21 +27,39 @@
 
 namespace vpcsum {
 
-static thread_local std::string g_err;
+// The thread's last error message: a fixed buffer, so that reporting a failure never allocates
+// (an out-of-memory failure must still leave its message)
+static thread_local char g_err[1024];
 
 static int fail(const char* fmt, ...) {
-    char buf[1024];
+    char buf[sizeof(g_err)];   // the arguments may point into g_err itself
     va_list ap;
     va_start(ap, fmt);
     vsnprintf(buf, sizeof(buf), fmt, ap);
     va_end(ap);
-    g_err = buf;
+    memcpy(g_err, buf, sizeof(g_err));
     return -1;
 }
 
 static int hipfail(hipError_t e, const char* what) {
     return fail("%s: %s (%d)", what, hipGetErrorString(e), (int)e);
 }
+
+// Every extern "C" entry point catches what the C++ runtime may throw (std::bad_alloc from the
+// bookkeeping containers, ...): an exception must never unwind into a C or JVM caller.  The entry
+// returns -1 with the message set (PNI: the exception stored in env->ex).
+#define VPC_CATCH(what)                                                                 \
+    catch (const std::bad_alloc&) { return fail("%s: out of host memory", what); }     \
+    catch (...) { return fail("%s: internal error (C++ exception)", what); }
+#define VPC_CATCH_PNI(what)                                                             \
+    catch (const std::bad_alloc&) {                                                     \
+        fail("%s: out of host memory", what);                                           \
+        return pni_throw(env, "java.lang.OutOfMemoryError");                            \
+    }                                                                                   \
+    catch (...) {                                                                       \
+        fail("%s: internal error (C++ exception)", what);                               \
+        return pni_throw(env, "java.io.IOException");                                   \
+    }
 
 #define VPC_CHECK(expr, what)                         \
     do {                                              \
@@ -185,19 +205,23 @@ extern "C" {
 
 int vpcsum_abi_version(void) { return VPCSUM_ABI_VERSION; }
 
-const char* vpcsum_last_error(void) { return g_err.c_str(); }
+const char* vpcsum_last_error(void) { return g_err; }
 
 int vpcsum_device_count(int* out_n) {
-    if (!out_n) return fail("vpcsum_device_count: out_n is NULL");
-    int n = 0;
-    VPC_CHECK(hipGetDeviceCount(&n), "hipGetDeviceCount");
-    *out_n = n;
-    return 0;
+    try {
+        if (!out_n) return fail("vpcsum_device_count: out_n is NULL");
+        int n = 0;
+        VPC_CHECK(hipGetDeviceCount(&n), "hipGetDeviceCount");
+        *out_n = n;
+        return 0;
+    } VPC_CATCH("vpcsum_device_count")
 }
 
 int vpcsum_set_device(int device) {
-    VPC_CHECK(hipSetDevice(device), "hipSetDevice");
-    return 0;
+    try {
+        VPC_CHECK(hipSetDevice(device), "hipSetDevice");
+        return 0;
+    } VPC_CATCH("vpcsum_set_device")
 }
 
 // kernel variant id: bits 8..12 low, bits 24..26 high (0..255; 0 = default)
@@ -205,23 +229,25 @@ static int team_from_mode(uint32_t mode) { return (int)(((mode >> 8) & 0x1f) | (
 
 int vpcsum_compute_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, uint32_t n,
                          uint32_t* d_out, uint8_t* d_status, uint32_t mode, void* stream) {
-    if (n == 0) return 0;
-    if (!d_arena || !d_desc) return fail("vpcsum_compute_async: NULL arena or descriptors");
-    // tuning hints (not part of the stable ABI): bits 8..12 + 24..26 kernel variant, bit 13
-    // plain (temporal) loads, bit 14 no sampled low-concurrency grid, bits 16..23 workgroups
-    // per CU.
-    if (mode & ~(0x07ff7fffu | VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_compute_async: bad mode 0x%x", mode);
-    uint8_t* w = (mode & VPCSUM_MODE_WRITE) ? const_cast<uint8_t*>(d_arena) : nullptr;
-    int grid = 0;
-    if ((mode >> 16) & 0xff) {
-        int dev = 0;
-        VPC_CHECK(hipGetDevice(&dev), "hipGetDevice");
-        grid = num_cus(dev) * (int)((mode >> 16) & 0xff);
-    }
-    VPC_CHECK(launch_csum(d_arena, arena_len, d_desc, n, d_out, d_status, nullptr, mode, w, team_from_mode(mode), grid,
-                          (hipStream_t)stream),
-              "vpcsum_compute_async launch");
-    return 0;
+    try {
+        if (n == 0) return 0;
+        if (!d_arena || !d_desc) return fail("vpcsum_compute_async: NULL arena or descriptors");
+        // tuning hints (not part of the stable ABI): bits 8..12 + 24..26 kernel variant, bit 13
+        // plain (temporal) loads, bit 14 no sampled low-concurrency grid, bits 16..23 workgroups
+        // per CU.
+        if (mode & ~(0x07ff7fffu | VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_compute_async: bad mode 0x%x", mode);
+        uint8_t* w = (mode & VPCSUM_MODE_WRITE) ? const_cast<uint8_t*>(d_arena) : nullptr;
+        int grid = 0;
+        if ((mode >> 16) & 0xff) {
+            int dev = 0;
+            VPC_CHECK(hipGetDevice(&dev), "hipGetDevice");
+            grid = num_cus(dev) * (int)((mode >> 16) & 0xff);
+        }
+        VPC_CHECK(launch_csum(d_arena, arena_len, d_desc, n, d_out, d_status, nullptr, mode, w, team_from_mode(mode), grid,
+                              (hipStream_t)stream),
+                  "vpcsum_compute_async launch");
+        return 0;
+    } VPC_CATCH("vpcsum_compute_async")
 }
 
 // NAT on device memory: the rewrite kernel, then (strict Java) the full recompute of the sums it
@@ -247,9 +273,10 @@ static int nat_async(const char* what, uint8_t* d_arena, uint64_t arena_len, con
                      const void* d_rw, int fmt, uint32_t n, uint8_t* d_status, uint32_t nat_mode, void* stream) {
     if (n == 0) return 0;
     if (!d_arena || !d_desc || !d_rw) return fail("%s: NULL arena, descriptors or rewrite table", what);
-    // tuning hints (not part of the stable ABI): bit 8 byte-access kernel, bits 12..14 packets
-    // per lane of the wide kernel, bits 16..17 window chunks, bits 18..22 workgroups per CU, bit 23
-    // the lane layout of the wide kernel instead of quads
+    // tuning hints (not part of the stable ABI; nat.hip, above nat_chunks_sel): bit 8 byte-access
+    // kernel, bits 12..14 packets per lane of the wide kernel (the quad kernel clamps 4 to 2), bits
+    // 16..17 window chunks, bits 18..22 workgroups per CU, bit 23 the lane layout of the wide kernel
+    // instead of quads, bits 24..25 the quad kernel's forced occupancy (6 / 8 waves: may spill)
     if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u | 0x7000u | 0x3ff0000u)) return fail("%s: bad nat_mode 0x%x", what, nat_mode);
     if ((nat_mode & VPCSUM_NAT_STRICT_JAVA) && !d_status) return fail("%s: strict-java mode needs a status buffer", what);
     return nat_run(d_arena, arena_len, d_desc, d_rw, fmt, n, d_status, nat_mode, (hipStream_t)stream);
@@ -257,102 +284,128 @@ static int nat_async(const char* what, uint8_t* d_arena, uint64_t arena_len, con
 
 int vpcsum_nat4_pattern_probe_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc,
                                     const vpcsum_nat4_t* d_rw, uint32_t n, void* stream) {
-    if (n == 0) return 0;
-    if (!d_arena || !d_desc || !d_rw) return fail("vpcsum_nat4_pattern_probe_async: NULL argument");
-    VPC_CHECK(launch_nat_probe(d_arena, arena_len, d_desc, d_rw, 0, n, (hipStream_t)stream),
-              "vpcsum_nat4_pattern_probe_async launch");
-    return 0;
+    try {
+        if (n == 0) return 0;
+        if (!d_arena || !d_desc || !d_rw) return fail("vpcsum_nat4_pattern_probe_async: NULL argument");
+        VPC_CHECK(launch_nat_probe(d_arena, arena_len, d_desc, d_rw, 0, n, (hipStream_t)stream),
+                  "vpcsum_nat4_pattern_probe_async launch");
+        return 0;
+    } VPC_CATCH("vpcsum_nat4_pattern_probe_async")
 }
 
 int vpcsum_nat4_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const vpcsum_nat4_t* d_rw,
                       uint32_t n, uint8_t* d_status, uint32_t nat_mode, void* stream) {
-    return nat_async("vpcsum_nat4_async", d_arena, arena_len, d_desc, d_rw, 0, n, d_status, nat_mode, stream);
+    try {
+        return nat_async("vpcsum_nat4_async", d_arena, arena_len, d_desc, d_rw, 0, n, d_status, nat_mode, stream);
+    } VPC_CATCH("vpcsum_nat4_async")
 }
 
 int vpcsum_nat_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const vpcsum_nat_t* d_rw,
                      uint32_t n, uint8_t* d_status, uint32_t nat_mode, void* stream) {
-    return nat_async("vpcsum_nat_async", d_arena, arena_len, d_desc, d_rw, 1, n, d_status, nat_mode, stream);
+    try {
+        return nat_async("vpcsum_nat_async", d_arena, arena_len, d_desc, d_rw, 1, n, d_status, nat_mode, stream);
+    } VPC_CATCH("vpcsum_nat_async")
 }
 
 int vpcsum_parse_ether_async(const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_frame_off,
                              const uint32_t* d_frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* d_desc,
                              uint8_t* d_status, void* stream) {
-    if (n == 0) return 0;
-    if (!d_arena || !d_frame_off || !d_frame_len || !d_desc) return fail("vpcsum_parse_ether_async: NULL argument");
-    VPC_CHECK(launch_parse_ether(d_arena, arena_len, d_frame_off, d_frame_len, n, flags, d_desc, d_status, nullptr,
-                                 (hipStream_t)stream),
-              "parse launch");
-    return 0;
+    try {
+        if (n == 0) return 0;
+        if (!d_arena || !d_frame_off || !d_frame_len || !d_desc) return fail("vpcsum_parse_ether_async: NULL argument");
+        VPC_CHECK(launch_parse_ether(d_arena, arena_len, d_frame_off, d_frame_len, n, flags, d_desc, d_status, nullptr,
+                                     (hipStream_t)stream),
+                  "parse launch");
+        return 0;
+    } VPC_CATCH("vpcsum_parse_ether_async")
 }
 
 int vpcsum_parse_ether_tuples_async(const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_frame_off,
                                     const uint32_t* d_frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* d_desc,
                                     uint8_t* d_status, vpcsum_tuple_t* d_tuples, void* stream) {
-    if (n == 0) return 0;
-    if (!d_arena || !d_frame_off || !d_frame_len || !d_desc || !d_tuples)
-        return fail("vpcsum_parse_ether_tuples_async: NULL argument");
-    if ((uintptr_t)d_tuples & 3) return fail("vpcsum_parse_ether_tuples_async: tuples not 4-byte aligned");
-    VPC_CHECK(launch_parse_ether(d_arena, arena_len, d_frame_off, d_frame_len, n, flags, d_desc, d_status, d_tuples,
-                                 (hipStream_t)stream),
-              "parse launch");
-    return 0;
+    try {
+        if (n == 0) return 0;
+        if (!d_arena || !d_frame_off || !d_frame_len || !d_desc || !d_tuples)
+            return fail("vpcsum_parse_ether_tuples_async: NULL argument");
+        if ((uintptr_t)d_tuples & 3) return fail("vpcsum_parse_ether_tuples_async: tuples not 4-byte aligned");
+        VPC_CHECK(launch_parse_ether(d_arena, arena_len, d_frame_off, d_frame_len, n, flags, d_desc, d_status, d_tuples,
+                                     (hipStream_t)stream),
+                  "parse launch");
+        return 0;
+    } VPC_CATCH("vpcsum_parse_ether_tuples_async")
 }
 
 int vpcsum_read_probe_async(const uint8_t* d_buf, uint64_t bytes, uint32_t* d_sink, uint32_t grid, void* stream) {
-    if (!d_buf || !d_sink) return fail("vpcsum_read_probe_async: NULL argument");
-    VPC_CHECK(launch_read_probe(d_buf, bytes, d_sink, grid, (hipStream_t)stream), "read probe launch");
-    return 0;
+    try {
+        if (!d_buf || !d_sink) return fail("vpcsum_read_probe_async: NULL argument");
+        VPC_CHECK(launch_read_probe(d_buf, bytes, d_sink, grid, (hipStream_t)stream), "read probe launch");
+        return 0;
+    } VPC_CATCH("vpcsum_read_probe_async")
 }
 
 int vpcsum_pattern_probe_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, uint32_t n,
                                uint32_t* d_sink, uint32_t grid, void* stream) {
-    if (n == 0) return 0;
-    if (!d_arena || !d_desc || !d_sink) return fail("vpcsum_pattern_probe_async: NULL argument");
-    if (arena_len >= (1ull << 32)) return fail("vpcsum_pattern_probe_async: arena must be < 4 GiB");
-    VPC_CHECK(launch_pattern_probe(d_arena, arena_len, d_desc, n, d_sink, grid, (hipStream_t)stream),
-              "pattern probe launch");
-    return 0;
+    try {
+        if (n == 0) return 0;
+        if (!d_arena || !d_desc || !d_sink) return fail("vpcsum_pattern_probe_async: NULL argument");
+        if (arena_len >= (1ull << 32)) return fail("vpcsum_pattern_probe_async: arena must be < 4 GiB");
+        VPC_CHECK(launch_pattern_probe(d_arena, arena_len, d_desc, n, d_sink, grid, (hipStream_t)stream),
+                  "pattern probe launch");
+        return 0;
+    } VPC_CATCH("vpcsum_pattern_probe_async")
 }
 
 int vpcsum_synth_async(uint8_t* d_arena, uint64_t arena_len, uint32_t n, uint32_t stride, uint32_t l3_pad,
                        uint32_t workload, uint64_t seed, uint64_t first_index, vpcsum_desc_t* d_desc, void* stream) {
-    if (n == 0) return 0;
-    if (!d_arena && !d_desc) return fail("vpcsum_synth_async: NULL arena and descriptors");
-    if (workload < VPCSUM_SYNTH_C1_UDP64 || workload > VPCSUM_SYNTH_C5_NAT1500) return fail("vpcsum_synth_async: bad workload %u", workload);
-    const uint32_t maxlen = (workload == VPCSUM_SYNTH_C4_V6JUMBO || workload == VPCSUM_SYNTH_FUZZ) ? 9000
-                            : (workload == VPCSUM_SYNTH_C1_UDP64) ? 50 : 1500;
-    if ((uint64_t)l3_pad + maxlen > stride) return fail("vpcsum_synth_async: stride %u < l3_pad %u + %u", stride, l3_pad, maxlen);
-    if (d_arena && (uint64_t)n * stride > arena_len) return fail("vpcsum_synth_async: arena too small");
-    VPC_CHECK(launch_synth(d_arena, arena_len, n, stride, l3_pad, workload, seed, first_index, d_desc,
-                           (hipStream_t)stream),
-              "synth launch");
-    return 0;
+    try {
+        if (n == 0) return 0;
+        if (!d_arena && !d_desc) return fail("vpcsum_synth_async: NULL arena and descriptors");
+        if (workload < VPCSUM_SYNTH_C1_UDP64 || workload > VPCSUM_SYNTH_C5_NAT1500) return fail("vpcsum_synth_async: bad workload %u", workload);
+        const uint32_t maxlen = (workload == VPCSUM_SYNTH_C4_V6JUMBO || workload == VPCSUM_SYNTH_FUZZ) ? 9000
+                                : (workload == VPCSUM_SYNTH_C1_UDP64) ? 50 : 1500;
+        if ((uint64_t)l3_pad + maxlen > stride) return fail("vpcsum_synth_async: stride %u < l3_pad %u + %u", stride, l3_pad, maxlen);
+        if (d_arena && (uint64_t)n * stride > arena_len) return fail("vpcsum_synth_async: arena too small");
+        VPC_CHECK(launch_synth(d_arena, arena_len, n, stride, l3_pad, workload, seed, first_index, d_desc,
+                               (hipStream_t)stream),
+                  "synth launch");
+        return 0;
+    } VPC_CATCH("vpcsum_synth_async")
 }
 
 int vpcsum_event_create(void** ev) {
-    if (!ev) return fail("vpcsum_event_create: NULL");
-    hipEvent_t e;
-    VPC_CHECK(hipEventCreate(&e), "hipEventCreate");
-    *ev = (void*)e;
-    return 0;
+    try {
+        if (!ev) return fail("vpcsum_event_create: NULL");
+        hipEvent_t e;
+        VPC_CHECK(hipEventCreate(&e), "hipEventCreate");
+        *ev = (void*)e;
+        return 0;
+    } VPC_CATCH("vpcsum_event_create")
 }
 int vpcsum_event_destroy(void* ev) {
-    VPC_CHECK(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy");
-    return 0;
+    try {
+        VPC_CHECK(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy");
+        return 0;
+    } VPC_CATCH("vpcsum_event_destroy")
 }
 int vpcsum_event_record(void* ev, void* stream) {
-    VPC_CHECK(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream), "hipEventRecord");
-    return 0;
+    try {
+        VPC_CHECK(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream), "hipEventRecord");
+        return 0;
+    } VPC_CATCH("vpcsum_event_record")
 }
 int vpcsum_event_elapsed_ms(void* start, void* end, float* ms) {
-    if (!ms) return fail("vpcsum_event_elapsed_ms: NULL");
-    VPC_CHECK(hipEventSynchronize((hipEvent_t)end), "hipEventSynchronize");
-    VPC_CHECK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end), "hipEventElapsedTime");
-    return 0;
+    try {
+        if (!ms) return fail("vpcsum_event_elapsed_ms: NULL");
+        VPC_CHECK(hipEventSynchronize((hipEvent_t)end), "hipEventSynchronize");
+        VPC_CHECK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end), "hipEventElapsedTime");
+        return 0;
+    } VPC_CATCH("vpcsum_event_elapsed_ms")
 }
 int vpcsum_stream_sync(void* stream) {
-    VPC_CHECK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
-    return 0;
+    try {
+        VPC_CHECK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+        return 0;
+    } VPC_CATCH("vpcsum_stream_sync")
 }
 
 // ------------------------------------------------------------------------------------------
@@ -395,135 +448,154 @@ static void svc_free(vpcsum_ctx* c) {
 }
 
 int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
-    if (!c) return fail("vpcsum_ctx_set_service: NULL context");
-    std::lock_guard<std::mutex> lk(c->mu);
-    VPC_ON_DEVICE(c->device);
-    for (auto& s : c->slots)
-        if (s.busy && slot_finish(c, s) != 0) return -1;
-    svc_free(c);
-    if (idle_us == 0) return 0;
-    if (c->max_pkts > kSvcMaxPkts) return fail("vpcsum_ctx_set_service: capacity %u > %u packets", c->max_pkts, kSvcMaxPkts);
-    Service& v = c->svc;
-    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-    hipError_t e = hipSuccess;
-    if ((e = hipHostMalloc((void**)&v.mb, sizeof(SvcMailbox), fl)) != hipSuccess ||
-        (e = hipHostGetDevicePointer((void**)&v.dmb, v.mb, 0)) != hipSuccess ||
-        (e = hipHostMalloc((void**)&v.h_desc, (size_t)c->max_pkts * sizeof(vpcsum_desc_t), fl)) != hipSuccess ||
-        (e = hipHostMalloc((void**)&v.h_out, (size_t)c->max_pkts * 4, fl)) != hipSuccess ||
-        (e = hipHostMalloc((void**)&v.h_status, (size_t)c->max_pkts, fl)) != hipSuccess ||
-        (e = hipHostGetDevicePointer((void**)&v.dh_desc, v.h_desc, 0)) != hipSuccess ||
-        (e = hipHostGetDevicePointer((void**)&v.dh_out, v.h_out, 0)) != hipSuccess ||
-        (e = hipHostGetDevicePointer((void**)&v.dh_status, v.h_status, 0)) != hipSuccess ||
-        (e = hipMalloc((void**)&v.ctr, 16)) != hipSuccess ||   // counter + command relay
-        (e = hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking)) != hipSuccess) {
+    try {
+        if (!c) return fail("vpcsum_ctx_set_service: NULL context");
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        for (auto& s : c->slots)
+            if (s.busy && slot_finish(c, s) != 0) return -1;
         svc_free(c);
-        return hipfail(e, "vpcsum_ctx_set_service allocation");
-    }
-    memset((void*)v.mb, 0, sizeof(SvcMailbox));
-    v.mb->desc = (uint64_t)(uintptr_t)v.dh_desc;
-    v.mb->out = (uint64_t)(uintptr_t)v.dh_out;
-    v.mb->status = (uint64_t)(uintptr_t)v.dh_status;
-    v.idle_ticks = (uint64_t)idle_us * 100u;   // s_memrealtime runs at 100 MHz
-    const char* inl = getenv("VPCSUM_SVC_INLINE");
-    v.inline_desc = !(inl && inl[0] == '0');
-    const char* clamp = getenv("VPCSUM_SVC_CLAMP");   // A/B tooling: 1 = clamped frame loads
-    const char* reld = getenv("VPCSUM_SVC_RELEASE_DONE");   // A/B tooling: 1 = release on count / done
-    v.mb->opts = ((clamp && clamp[0] == '1') ? kSvcOptClampLoads : 0) | ((reld && reld[0] == '1') ? kSvcOptReleaseDone : 0);
-    v.on = true;
-    return 0;
+        if (idle_us == 0) return 0;
+        if (c->max_pkts > kSvcMaxPkts) return fail("vpcsum_ctx_set_service: capacity %u > %u packets", c->max_pkts, kSvcMaxPkts);
+        Service& v = c->svc;
+        const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+        hipError_t e = hipSuccess;
+        if ((e = hipHostMalloc((void**)&v.mb, sizeof(SvcMailbox), fl)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&v.dmb, v.mb, 0)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&v.h_desc, (size_t)c->max_pkts * sizeof(vpcsum_desc_t), fl)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&v.h_out, (size_t)c->max_pkts * 4, fl)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&v.h_status, (size_t)c->max_pkts, fl)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&v.dh_desc, v.h_desc, 0)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&v.dh_out, v.h_out, 0)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&v.dh_status, v.h_status, 0)) != hipSuccess ||
+            (e = hipMalloc((void**)&v.ctr, 16)) != hipSuccess ||   // counter + command relay
+            (e = hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking)) != hipSuccess) {
+            svc_free(c);
+            return hipfail(e, "vpcsum_ctx_set_service allocation");
+        }
+        memset((void*)v.mb, 0, sizeof(SvcMailbox));
+        v.mb->desc = (uint64_t)(uintptr_t)v.dh_desc;
+        v.mb->out = (uint64_t)(uintptr_t)v.dh_out;
+        v.mb->status = (uint64_t)(uintptr_t)v.dh_status;
+        v.idle_ticks = (uint64_t)idle_us * 100u;   // s_memrealtime runs at 100 MHz
+        const char* inl = getenv("VPCSUM_SVC_INLINE");
+        v.inline_desc = !(inl && inl[0] == '0');
+        const char* clamp = getenv("VPCSUM_SVC_CLAMP");   // A/B tooling: 1 = clamped frame loads
+        const char* reld = getenv("VPCSUM_SVC_RELEASE_DONE");   // A/B tooling: 1 = release on count / done
+        v.mb->opts = ((clamp && clamp[0] == '1') ? kSvcOptClampLoads : 0) | ((reld && reld[0] == '1') ? kSvcOptReleaseDone : 0);
+        v.on = true;
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_set_service")
 }
 
 int vpcsum_ctx_stats(vpcsum_ctx_t* c, uint64_t* service_batches, uint64_t* service_launches) {
-    if (!c) return fail("vpcsum_ctx_stats: NULL context");
-    std::lock_guard<std::mutex> lk(c->mu);
-    if (service_batches) *service_batches = c->svc_batches;
-    if (service_launches) *service_launches = c->svc_launches;
-    return 0;
+    try {
+        if (!c) return fail("vpcsum_ctx_stats: NULL context");
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (service_batches) *service_batches = c->svc_batches;
+        if (service_launches) *service_launches = c->svc_launches;
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_stats")
 }
 
 int vpcsum_ctx_create(int device, uint64_t max_arena_bytes, uint32_t max_pkts, vpcsum_ctx_t** out) {
-    if (!out) return fail("vpcsum_ctx_create: out is NULL");
-    if (max_arena_bytes == 0 || max_pkts == 0) return fail("vpcsum_ctx_create: zero capacity");
-    VPC_ON_DEVICE(device);
-    vpcsum_ctx* c = new vpcsum_ctx();
-    c->device = device;
-    c->max_arena = max_arena_bytes;
-    c->max_pkts = max_pkts;
-    for (auto& s : c->slots) {
-        hipError_t e = hipSuccess;
-        if ((e = hipMalloc((void**)&s.d_arena, max_arena_bytes + 64)) != hipSuccess ||
-            (e = hipMalloc((void**)&s.d_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t))) != hipSuccess ||
-            (e = hipMalloc((void**)&s.d_out, (size_t)max_pkts * 4)) != hipSuccess ||
-            (e = hipMalloc((void**)&s.d_status, (size_t)max_pkts)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_out, (size_t)max_pkts * 4, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_status, (size_t)max_pkts, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
-            (e = hipHostGetDevicePointer((void**)&s.dh_desc, s.h_desc, 0)) != hipSuccess ||
-            (e = hipHostGetDevicePointer((void**)&s.dh_out, s.h_out, 0)) != hipSuccess ||
-            (e = hipHostGetDevicePointer((void**)&s.dh_status, s.h_status, 0)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_arena, max_arena_bytes + 64, 0)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_foff, (size_t)max_pkts * 8, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&s.h_flen, (size_t)max_pkts * 4, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
-            (e = hipHostGetDevicePointer((void**)&s.dh_foff, s.h_foff, 0)) != hipSuccess ||
-            (e = hipHostGetDevicePointer((void**)&s.dh_flen, s.h_flen, 0)) != hipSuccess ||
-            (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
-            for (auto& t : c->slots) slot_free(t);
-            delete c;
-            return hipfail(e, "vpcsum_ctx_create allocation");
+    try {
+        if (!out) return fail("vpcsum_ctx_create: out is NULL");
+        if (max_arena_bytes == 0 || max_pkts == 0) return fail("vpcsum_ctx_create: zero capacity");
+        VPC_ON_DEVICE(device);
+        vpcsum_ctx* c = new vpcsum_ctx();
+        c->device = device;
+        c->max_arena = max_arena_bytes;
+        c->max_pkts = max_pkts;
+        for (auto& s : c->slots) {
+            hipError_t e = hipSuccess;
+            if ((e = hipMalloc((void**)&s.d_arena, max_arena_bytes + 64)) != hipSuccess ||
+                (e = hipMalloc((void**)&s.d_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t))) != hipSuccess ||
+                (e = hipMalloc((void**)&s.d_out, (size_t)max_pkts * 4)) != hipSuccess ||
+                (e = hipMalloc((void**)&s.d_status, (size_t)max_pkts)) != hipSuccess ||
+                (e = hipHostMalloc((void**)&s.h_desc, (size_t)max_pkts * sizeof(vpcsum_desc_t), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+                (e = hipHostMalloc((void**)&s.h_out, (size_t)max_pkts * 4, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+                (e = hipHostMalloc((void**)&s.h_status, (size_t)max_pkts, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+                (e = hipHostGetDevicePointer((void**)&s.dh_desc, s.h_desc, 0)) != hipSuccess ||
+                (e = hipHostGetDevicePointer((void**)&s.dh_out, s.h_out, 0)) != hipSuccess ||
+                (e = hipHostGetDevicePointer((void**)&s.dh_status, s.h_status, 0)) != hipSuccess ||
+                (e = hipHostMalloc((void**)&s.h_arena, max_arena_bytes + 64, 0)) != hipSuccess ||
+                (e = hipHostMalloc((void**)&s.h_foff, (size_t)max_pkts * 8, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+                (e = hipHostMalloc((void**)&s.h_flen, (size_t)max_pkts * 4, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+                (e = hipHostGetDevicePointer((void**)&s.dh_foff, s.h_foff, 0)) != hipSuccess ||
+                (e = hipHostGetDevicePointer((void**)&s.dh_flen, s.h_flen, 0)) != hipSuccess ||
+                (e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
+                for (auto& t : c->slots) slot_free(t);
+                delete c;
+                return hipfail(e, "vpcsum_ctx_create allocation");
+            }
         }
-    }
-    *out = c;
-    return 0;
+        *out = c;
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_create")
 }
 
 int vpcsum_ctx_destroy(vpcsum_ctx_t* c) {
-    if (!c) return 0;
-    DeviceScope on_dev(c->device);
-    svc_free(c);
-    for (auto& s : c->slots) {
-        if (s.stream) (void)hipStreamSynchronize(s.stream);
-        slot_free(s);
-    }
-    for (auto& r : c->registered)
-        if (r.owned) (void)hipHostUnregister(r.host);
-    delete c;
-    return 0;
+    try {
+        if (!c) return 0;
+        DeviceScope on_dev(c->device);
+        svc_free(c);
+        for (auto& s : c->slots) {
+            if (s.stream) (void)hipStreamSynchronize(s.stream);
+            slot_free(s);
+        }
+        for (auto& r : c->registered)
+            if (r.owned) (void)hipHostUnregister(r.host);
+        delete c;
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_destroy")
 }
 
 int vpcsum_ctx_register_arena(vpcsum_ctx_t* c, void* h_arena, uint64_t len) {
-    if (!c || !h_arena || len == 0) return fail("vpcsum_ctx_register_arena: bad argument");
-    std::lock_guard<std::mutex> lk(c->mu);
-    VPC_ON_DEVICE(c->device);
-    VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterMapped), "hipHostRegister");
-    void* dev = nullptr;
-    hipError_t e = hipHostGetDevicePointer(&dev, h_arena, 0);
-    if (e != hipSuccess) {
-        (void)hipHostUnregister(h_arena);
-        return hipfail(e, "hipHostGetDevicePointer");
-    }
-    c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, true});
+    try {
+        if (!c || !h_arena || len == 0) return fail("vpcsum_ctx_register_arena: bad argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        c->registered.reserve(c->registered.size() + 1);   // may throw: before anything is pinned
+        VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterMapped), "hipHostRegister");
+        void* dev = nullptr;
+        hipError_t e = hipHostGetDevicePointer(&dev, h_arena, 0);
+        if (e != hipSuccess) {
+            (void)hipHostUnregister(h_arena);
+            return hipfail(e, "hipHostGetDevicePointer");
+        }
+        c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, true});
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_register_arena")
+}
+
+// A zero-copy batch (launched or on the service grid) may still read and write frames of a
+// registered arena in place: finish every such batch of the context before a mapping goes away,
+// and make the service re-read its parameters (they may name that arena) with its next batch.
+// Caller holds c->mu on c's device.
+static int ctx_quiesce_zero_copy(vpcsum_ctx* c) {
+    for (auto& s : c->slots)
+        if (s.busy && s.zero_copy && slot_finish(c, s) != 0) return -1;
+    c->svc.par_valid = false;
     return 0;
 }
 
 int vpcsum_ctx_unregister_arena(vpcsum_ctx_t* c, void* h_arena) {
-    if (!c || !h_arena) return fail("vpcsum_ctx_unregister_arena: bad argument");
-    std::lock_guard<std::mutex> lk(c->mu);
-    VPC_ON_DEVICE(c->device);
-    for (size_t i = 0; i < c->registered.size(); ++i) {
-        if (c->registered[i].host == (uint8_t*)h_arena) {
-            // a zero-copy batch (launched or on the service grid) may still read and write the
-            // frames in place: finish every such batch before the mapping goes away, and make the
-            // service re-read its parameters (they name this arena) with its next batch
-            for (auto& s : c->slots)
-                if (s.busy && s.zero_copy && slot_finish(c, s) != 0) return -1;
-            c->svc.par_valid = false;
-            if (c->registered[i].owned) VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
-            c->registered.erase(c->registered.begin() + i);
-            return 0;
+    try {
+        if (!c || !h_arena) return fail("vpcsum_ctx_unregister_arena: bad argument");
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        for (size_t i = 0; i < c->registered.size(); ++i) {
+            if (c->registered[i].host == (uint8_t*)h_arena) {
+                if (ctx_quiesce_zero_copy(c) != 0) return -1;
+                if (c->registered[i].owned) VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
+                c->registered.erase(c->registered.begin() + i);
+                return 0;
+            }
         }
-    }
-    return fail("vpcsum_ctx_unregister_arena: arena not registered");
+        return fail("vpcsum_ctx_unregister_arena: arena not registered");
+    } VPC_CATCH("vpcsum_ctx_unregister_arena")
 }
 
 // Device-side address of host range [p, p+len) if it lies in an arena registered with this context.
@@ -665,110 +737,362 @@ static int slot_finish(vpcsum_ctx* c, Slot& s) {
 
 int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, uint32_t n,
                       uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket) {
-    if (!c || !ticket) return fail("vpcsum_ctx_submit: NULL context or ticket");
-    if (n > c->max_pkts) return fail("vpcsum_ctx_submit: %u packets > capacity %u", n, c->max_pkts);
-    if (n && (!h_arena || !h_desc)) return fail("vpcsum_ctx_submit: NULL arena or descriptors");
-    if (mode & ~(VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_ctx_submit: bad mode 0x%x", mode);
-    std::lock_guard<std::mutex> lk(c->mu);
-    VPC_ON_DEVICE(c->device);
-    const uint64_t t = c->next_ticket++;
-    Slot& s = c->slots[t & 1];
-    if (s.busy && slot_finish(c, s) != 0) return -1;
+    try {
+        if (!c || !ticket) return fail("vpcsum_ctx_submit: NULL context or ticket");
+        if (n > c->max_pkts) return fail("vpcsum_ctx_submit: %u packets > capacity %u", n, c->max_pkts);
+        if (n && (!h_arena || !h_desc)) return fail("vpcsum_ctx_submit: NULL arena or descriptors");
+        if (mode & ~(VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_ctx_submit: bad mode 0x%x", mode);
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        const uint64_t t = c->next_ticket++;
+        Slot& s = c->slots[t & 1];
+        if (s.busy && slot_finish(c, s) != 0) return -1;
 
-    // byte span the descriptors touch (16-B aligned so device alignment == host alignment)
-    uint64_t lo = UINT64_MAX, hi = 0, used = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const vpcsum_desc_t& d = h_desc[i];
-        if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) continue;   // kernel flags it BAD
-        lo = std::min(lo, d.l3_off);
-        hi = std::max(hi, d.l3_off + d.l3_len);
-        used += d.l3_len + 16;
-    }
-    if (lo == UINT64_MAX) { lo = 0; hi = 0; }
-    lo &= ~(uint64_t)15;
-    const uint64_t span = hi - lo;
-    s.zero_copy = false;
-
-    uint8_t* dev_arena = span ? mapped_dev(c, h_arena + lo, span) : nullptr;
-    if (dev_arena) {
-        // Zero-copy: the frames live in a page-locked, mapped arena (an AF_XDP umem).  The
-        // kernel reads them over PCIe in place, takes the descriptors from and writes the
-        // results to pinned staging, and with MODE_WRITE stores the checksum fields straight
-        // into the frames -- no DMA copy in either direction.
-        uint8_t* base = dev_arena - lo;   // device address of h_arena[0]
-        Service& v = c->svc;
-        if (v.on && n <= kSvcBatchMax) {
-            // low-latency service: one batch at a time; descriptors into the service's buffer,
-            // the parameter block if it changed, then the command word
-            for (auto& o : c->slots)   // the previous service batch: done, results handed over
-                if (o.busy && o.svc_seq && slot_finish(c, o) != 0) return -1;
-            SvcMailbox* mb = v.mb;
-            memcpy(v.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
-            const uint64_t par[3] = {(uint64_t)(uintptr_t)base, arena_len,
-                                     (mode & VPCSUM_MODE_WRITE) ? (uint64_t)(uintptr_t)base : 0};
-            uint64_t cmd = 0;
-            if (!v.par_valid || memcmp(par, v.par, sizeof(par)) != 0) {
-                mb->arena = par[0];
-                mb->arena_len = par[1];
-                mb->arena_w = par[2];
-                memcpy(v.par, par, sizeof(par));
-                v.par_valid = true;
-                cmd |= kSvcParams;
-            }
-            const uint32_t seq = v.posted + 1 ? v.posted + 1 : 1;
-            // the first descriptors ride in the command's line, tagged with the batch.  All of
-            // them are rewritten for every batch, so a stale one always carries the previous
-            // batch's tag; the high word (with the tag) is stored after the low one.
-            for (int k = 0; k < kSvcInlineDesc; ++k) {
-                vpcsum_desc_t d;
-                if ((uint32_t)k < n) memcpy(&d, &h_desc[k], sizeof(d));
-                else memset(&d, 0, sizeof(d));
-                d.rsv = (uint8_t)seq;
-                uint64_t w[2];
-                memcpy(w, &d, sizeof(w));
-                uint64_t* dst = reinterpret_cast<uint64_t*>(&mb->idesc[k]);
-                __atomic_store_n(&dst[0], w[0], __ATOMIC_RELAXED);
-                __atomic_store_n(&dst[1], w[1], __ATOMIC_RELEASE);
-            }
-            cmd |= seq | ((uint64_t)n << 32) | ((mode & VPCSUM_MODE_VERIFY) ? kSvcVerify : 0) |
-                   (v.inline_desc && n <= (uint32_t)kSvcInlineDesc ? kSvcInline : 0);
-#ifdef VPCSUM_SVC_STAMPS
-            v.t_post = std::chrono::steady_clock::now();
-            v.t_n = n;
-#endif
-            __atomic_store_n(&mb->cmd, cmd, __ATOMIC_RELEASE);
-            v.posted = seq;
-            ++c->svc_batches;
-            if (hipStreamQuery(v.stream) == hipSuccess && svc_launch(c, seq - 1) != 0) return -1;
-            s.zero_copy = true;
-            s.svc_seq = seq;
-            s.kind = 0;
-            s.busy = true;
-            s.ticket = t;
-            s.n = n;
-            s.mode = mode;
-            s.user_arena = h_arena;
-            s.user_desc = h_desc;
-            s.user_out = h_out;
-            s.user_status = h_status;
-            *ticket = t;
-            return 0;
+        // byte span the descriptors touch (16-B aligned so device alignment == host alignment)
+        uint64_t lo = UINT64_MAX, hi = 0, used = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const vpcsum_desc_t& d = h_desc[i];
+            if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) continue;   // kernel flags it BAD
+            lo = std::min(lo, d.l3_off);
+            hi = std::max(hi, d.l3_off + d.l3_len);
+            used += d.l3_len + 16;
         }
-        memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
-        // up to kZeroCopyWaveTeams packets: one wave per packet (variant 12, 64 lanes x 4
-        // predicated loads), so the batch is a few PCIe round trips deep instead of K2's per-unit
-        // iterations, and no chunk is read twice over PCIe
-        const int variant = n <= kZeroCopyWaveTeams ? 12 : 0;
-        VPC_CHECK(launch_csum(base, arena_len, s.dh_desc, n, s.dh_out, s.dh_status, nullptr,
-                              mode & VPCSUM_MODE_VERIFY, (mode & VPCSUM_MODE_WRITE) ? base : nullptr, variant, 0,
-                              s.stream),
-                  "checksum launch (zero-copy)");
+        if (lo == UINT64_MAX) { lo = 0; hi = 0; }
+        lo &= ~(uint64_t)15;
+        const uint64_t span = hi - lo;
+        s.zero_copy = false;
+
+        uint8_t* dev_arena = span ? mapped_dev(c, h_arena + lo, span) : nullptr;
+        if (dev_arena) {
+            // Zero-copy: the frames live in a page-locked, mapped arena (an AF_XDP umem).  The
+            // kernel reads them over PCIe in place, takes the descriptors from and writes the
+            // results to pinned staging, and with MODE_WRITE stores the checksum fields straight
+            // into the frames -- no DMA copy in either direction.
+            uint8_t* base = dev_arena - lo;   // device address of h_arena[0]
+            Service& v = c->svc;
+            if (v.on && n <= kSvcBatchMax) {
+                // low-latency service: one batch at a time; descriptors into the service's buffer,
+                // the parameter block if it changed, then the command word
+                for (auto& o : c->slots)   // the previous service batch: done, results handed over
+                    if (o.busy && o.svc_seq && slot_finish(c, o) != 0) return -1;
+                SvcMailbox* mb = v.mb;
+                memcpy(v.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
+                const uint64_t par[3] = {(uint64_t)(uintptr_t)base, arena_len,
+                                         (mode & VPCSUM_MODE_WRITE) ? (uint64_t)(uintptr_t)base : 0};
+                uint64_t cmd = 0;
+                if (!v.par_valid || memcmp(par, v.par, sizeof(par)) != 0) {
+                    mb->arena = par[0];
+                    mb->arena_len = par[1];
+                    mb->arena_w = par[2];
+                    memcpy(v.par, par, sizeof(par));
+                    v.par_valid = true;
+                    cmd |= kSvcParams;
+                }
+                const uint32_t seq = v.posted + 1 ? v.posted + 1 : 1;
+                // the first descriptors ride in the command's line, tagged with the batch.  All of
+                // them are rewritten for every batch, so a stale one always carries the previous
+                // batch's tag; the high word (with the tag) is stored after the low one.
+                for (int k = 0; k < kSvcInlineDesc; ++k) {
+                    vpcsum_desc_t d;
+                    if ((uint32_t)k < n) memcpy(&d, &h_desc[k], sizeof(d));
+                    else memset(&d, 0, sizeof(d));
+                    d.rsv = (uint8_t)seq;
+                    uint64_t w[2];
+                    memcpy(w, &d, sizeof(w));
+                    uint64_t* dst = reinterpret_cast<uint64_t*>(&mb->idesc[k]);
+                    __atomic_store_n(&dst[0], w[0], __ATOMIC_RELAXED);
+                    __atomic_store_n(&dst[1], w[1], __ATOMIC_RELEASE);
+                }
+                cmd |= seq | ((uint64_t)n << 32) | ((mode & VPCSUM_MODE_VERIFY) ? kSvcVerify : 0) |
+                       (v.inline_desc && n <= (uint32_t)kSvcInlineDesc ? kSvcInline : 0);
+    #ifdef VPCSUM_SVC_STAMPS
+                v.t_post = std::chrono::steady_clock::now();
+                v.t_n = n;
+    #endif
+                __atomic_store_n(&mb->cmd, cmd, __ATOMIC_RELEASE);
+                v.posted = seq;
+                ++c->svc_batches;
+                if (hipStreamQuery(v.stream) == hipSuccess && svc_launch(c, seq - 1) != 0) return -1;
+                s.zero_copy = true;
+                s.svc_seq = seq;
+                s.kind = 0;
+                s.busy = true;
+                s.ticket = t;
+                s.n = n;
+                s.mode = mode;
+                s.user_arena = h_arena;
+                s.user_desc = h_desc;
+                s.user_out = h_out;
+                s.user_status = h_status;
+                *ticket = t;
+                return 0;
+            }
+            memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
+            // up to kZeroCopyWaveTeams packets: one wave per packet (variant 12, 64 lanes x 4
+            // predicated loads), so the batch is a few PCIe round trips deep instead of K2's per-unit
+            // iterations, and no chunk is read twice over PCIe
+            const int variant = n <= kZeroCopyWaveTeams ? 12 : 0;
+            VPC_CHECK(launch_csum(base, arena_len, s.dh_desc, n, s.dh_out, s.dh_status, nullptr,
+                                  mode & VPCSUM_MODE_VERIFY, (mode & VPCSUM_MODE_WRITE) ? base : nullptr, variant, 0,
+                                  s.stream),
+                      "checksum launch (zero-copy)");
+            s.zero_copy = true;
+        } else {
+            const bool gather = span > 2 * used + (64u << 10);
+            uint64_t dev_len = span;
+            if (gather) {
+                // sparse batch in a large pageable arena: gather the touched 16-B blocks only
+                uint64_t pos = 0;
+                for (uint32_t i = 0; i < n; ++i) {
+                    const vpcsum_desc_t& d = h_desc[i];
+                    s.h_desc[i] = d;
+                    if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) { s.h_desc[i].l3_off = UINT64_MAX; continue; }
+                    const uint64_t a0 = d.l3_off & ~(uint64_t)15;
+                    const uint64_t a1 = std::min<uint64_t>((d.l3_off + d.l3_len + 15) & ~(uint64_t)15, arena_len);
+                    if (pos + (a1 - a0) > c->max_arena) return fail("vpcsum_ctx_submit: gathered batch exceeds capacity");
+                    memcpy(s.h_arena + pos, h_arena + a0, a1 - a0);
+                    s.h_desc[i].l3_off = pos + (d.l3_off - a0);
+                    pos += (a1 - a0 + 15) & ~(uint64_t)15;
+                }
+                dev_len = pos;
+            } else {
+                if (span > c->max_arena) return fail("vpcsum_ctx_submit: batch spans %llu bytes > capacity %llu",
+                                                     (unsigned long long)span, (unsigned long long)c->max_arena);
+                // descriptors rebased to the device copy of [lo, hi)
+                for (uint32_t i = 0; i < n; ++i) {
+                    s.h_desc[i] = h_desc[i];
+                    if (h_desc[i].l3_off >= lo) s.h_desc[i].l3_off = h_desc[i].l3_off - lo;
+                    else s.h_desc[i].l3_off = UINT64_MAX;   // out of span -> BAD in the kernel
+                }
+            }
+            VPC_CHECK(hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)n * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice, s.stream),
+                      "H2D descriptors");
+            if (dev_len) {
+                const uint8_t* src = gather ? s.h_arena : h_arena + lo;
+                if (!gather && !is_registered(c, src, span)) {
+                    memcpy(s.h_arena, src, span);   // pageable -> pinned staging
+                    src = s.h_arena;
+                }
+                VPC_CHECK(hipMemcpyAsync(s.d_arena, src, dev_len, hipMemcpyHostToDevice, s.stream), "H2D arena");
+            }
+            VPC_CHECK(launch_csum(s.d_arena, dev_len, s.d_desc, n, s.d_out, s.d_status, nullptr, mode & VPCSUM_MODE_VERIFY,
+                                  nullptr, 0, 0, s.stream),
+                      "checksum launch");
+            VPC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream), "D2H out");
+            VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
+        }
+        VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+        s.kind = 0;
+        s.busy = true;
+        s.ticket = t;
+        s.n = n;
+        s.mode = mode;
+        s.user_arena = h_arena;
+        s.user_desc = h_desc;
+        s.user_out = h_out;
+        s.user_status = h_status;
+        *ticket = t;
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_submit")
+}
+
+int vpcsum_ctx_wait(vpcsum_ctx_t* c, uint64_t ticket) {
+    try {
+        if (!c) return fail("vpcsum_ctx_wait: NULL context");
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        Slot& s = c->slots[ticket & 1];
+        if (!s.busy || s.ticket != ticket) {
+            if (ticket == 0 || ticket >= c->next_ticket) return fail("vpcsum_ctx_wait: unknown ticket %llu", (unsigned long long)ticket);
+            return 0;   // already completed
+        }
+        return slot_finish(c, s);
+    } VPC_CATCH("vpcsum_ctx_wait")
+}
+
+int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
+                             const uint32_t* h_frame_len, uint32_t n, uint32_t* h_out, uint8_t* h_status,
+                             uint64_t* ticket) {
+    try {
+        if (!c || !ticket) return fail("vpcsum_ctx_verify_frames: NULL context or ticket");
+        if (n > c->max_pkts) return fail("vpcsum_ctx_verify_frames: %u frames > capacity %u", n, c->max_pkts);
+        if (n && (!h_arena || !h_frame_off || !h_frame_len || !h_status))
+            return fail("vpcsum_ctx_verify_frames: NULL arena, frame table or status");
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
+        if (n && !base) return fail("vpcsum_ctx_verify_frames: the arena must be registered (vpcsum_ctx_register_arena)");
+        const uint64_t t = c->next_ticket++;
+        Slot& s = c->slots[t & 1];
+        if (s.busy && slot_finish(c, s) != 0) return -1;
+        if (n) {
+            // parse the frames where they lie (zero-copy), then verify the descriptors it built
+            memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
+            memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
+            VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.d_desc,
+                                         nullptr, nullptr, s.stream),
+                      "parse launch");
+            VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, s.dh_out, s.dh_status, nullptr, VPCSUM_MODE_VERIFY, nullptr,
+                                  n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
+                      "verify launch");
+        }
+        VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
         s.zero_copy = true;
-    } else {
-        const bool gather = span > 2 * used + (64u << 10);
-        uint64_t dev_len = span;
-        if (gather) {
-            // sparse batch in a large pageable arena: gather the touched 16-B blocks only
+        s.svc_seq = 0;
+        s.kind = 0;
+        s.busy = true;
+        s.ticket = t;
+        s.n = n;
+        s.mode = VPCSUM_MODE_VERIFY;
+        s.user_arena = nullptr;
+        s.user_desc = nullptr;
+        s.user_out = h_out;
+        s.user_status = h_status;
+        *ticket = t;
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_verify_frames")
+}
+
+int vpcsum_ctx_egress_frames(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
+                             const uint32_t* h_frame_len, const uint8_t* h_frame_flags, uint32_t n, uint32_t* h_out,
+                             uint8_t* h_status, uint64_t* ticket) {
+    try {
+        if (!c || !ticket) return fail("vpcsum_ctx_egress_frames: NULL context or ticket");
+        if (n > c->max_pkts) return fail("vpcsum_ctx_egress_frames: %u frames > capacity %u", n, c->max_pkts);
+        if (n && (!h_arena || !h_frame_off || !h_frame_len || !h_frame_flags))
+            return fail("vpcsum_ctx_egress_frames: NULL arena, frame table or flags");
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
+        if (n && !base) return fail("vpcsum_ctx_egress_frames: the arena must be registered (vpcsum_ctx_register_arena)");
+        const uint64_t t = c->next_ticket++;
+        Slot& s = c->slots[t & 1];
+        if (s.busy && slot_finish(c, s) != 0) return -1;
+        if (n) {
+            // the frames' own flags ride in the status staging: the parse reads them before the
+            // checksum kernel, later on the same stream, overwrites them with the statuses
+            memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
+            memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
+            memcpy(s.h_status, h_frame_flags, n);
+            VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, 0, s.d_desc, nullptr, nullptr, s.stream,
+                                         s.dh_status),
+                      "parse launch");
+            VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, s.dh_out, s.dh_status, nullptr, VPCSUM_MODE_COMPUTE, base,
+                                  n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
+                      "checksum launch");
+        }
+        VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+        s.zero_copy = true;
+        s.svc_seq = 0;
+        s.kind = 0;
+        s.busy = true;
+        s.ticket = t;
+        s.n = n;
+        s.mode = VPCSUM_MODE_WRITE;
+        s.user_arena = nullptr;   // written in place through the mapping
+        s.user_desc = nullptr;
+        s.user_out = h_out;
+        s.user_status = h_status;
+        *ticket = t;
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_egress_frames")
+}
+
+int vpcsum_ctx_parse_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
+                            const uint32_t* h_frame_len, uint32_t n, vpcsum_desc_t* h_desc, uint8_t* h_status,
+                            vpcsum_tuple_t* h_tuples, uint64_t* ticket) {
+    try {
+        if (!c || !ticket) return fail("vpcsum_ctx_parse_frames: NULL context or ticket");
+        if (n > c->max_pkts) return fail("vpcsum_ctx_parse_frames: %u frames > capacity %u", n, c->max_pkts);
+        if (n && (!h_arena || !h_frame_off || !h_frame_len)) return fail("vpcsum_ctx_parse_frames: NULL arena or frame table");
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
+        if (n && !base) return fail("vpcsum_ctx_parse_frames: the arena must be registered (vpcsum_ctx_register_arena)");
+        const uint64_t t = c->next_ticket++;
+        Slot& s = c->slots[t & 1];
+        if (s.busy && slot_finish(c, s) != 0) return -1;
+        if (!s.h_tu) {
+            hipError_t e = hipHostMalloc((void**)&s.h_tu, (size_t)c->max_pkts * sizeof(vpcsum_tuple_t),
+                                         hipHostMallocMapped | hipHostMallocCoherent);
+            if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s.dh_tu, s.h_tu, 0);
+            if (e != hipSuccess) {
+                if (s.h_tu) (void)hipHostFree(s.h_tu);
+                s.h_tu = s.dh_tu = nullptr;
+                return hipfail(e, "vpcsum_ctx_parse_frames allocation");
+            }
+        }
+        if (n) {
+            // parsed where the frames lie (zero-copy); results straight into the pinned staging
+            memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
+            memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
+            VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.dh_desc,
+                                         s.dh_status, s.dh_tu, s.stream),
+                      "parse launch");
+        }
+        VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+        s.zero_copy = true;
+        s.svc_seq = 0;
+        s.kind = 2;
+        s.busy = true;
+        s.ticket = t;
+        s.n = n;
+        s.mode = 0;
+        s.user_arena = nullptr;
+        s.user_desc = nullptr;
+        s.user_out = nullptr;
+        s.user_status = h_status;
+        s.user_desc_out = h_desc;
+        s.user_tuples = h_tuples;
+        *ticket = t;
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_parse_frames")
+}
+
+int vpcsum_ctx_nat_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                          const vpcsum_nat_t* h_rw, uint32_t n, uint8_t* h_status, uint32_t nat_mode, uint64_t* ticket) {
+    try {
+        if (!c || !ticket) return fail("vpcsum_ctx_nat_submit: NULL context or ticket");
+        if (n > c->max_pkts) return fail("vpcsum_ctx_nat_submit: %u packets > capacity %u", n, c->max_pkts);
+        if (n && (!h_arena || !h_desc || !h_rw)) return fail("vpcsum_ctx_nat_submit: NULL arena, descriptors or rewrites");
+        if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u)) return fail("vpcsum_ctx_nat_submit: bad nat_mode 0x%x", nat_mode);
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        const uint64_t t = c->next_ticket++;
+        Slot& s = c->slots[t & 1];
+        if (s.busy && slot_finish(c, s) != 0) return -1;
+        if (!s.h_rw) {
+            hipError_t e = hipSuccess;
+            const size_t bytes = (size_t)c->max_pkts * sizeof(vpcsum_nat_t);
+            if ((e = hipHostMalloc((void**)&s.h_rw, bytes, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+                (e = hipHostGetDevicePointer((void**)&s.dh_rw, s.h_rw, 0)) != hipSuccess ||
+                (e = hipMalloc((void**)&s.d_rw, bytes)) != hipSuccess) {
+                if (s.h_rw) (void)hipHostFree(s.h_rw);
+                if (s.d_rw) (void)hipFree(s.d_rw);
+                s.h_rw = s.dh_rw = s.d_rw = nullptr;
+                return hipfail(e, "vpcsum_ctx_nat_submit allocation");
+            }
+        }
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const vpcsum_desc_t& d = h_desc[i];
+            if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) continue;   // the kernel flags it BAD
+            lo = std::min(lo, d.l3_off);
+            hi = std::max(hi, d.l3_off + d.l3_len);
+        }
+        if (lo == UINT64_MAX) { lo = 0; hi = 0; }
+        lo &= ~(uint64_t)15;
+        uint8_t* dev_arena = hi > lo ? mapped_dev(c, h_arena + lo, hi - lo) : nullptr;
+        memcpy(s.h_rw, h_rw, (size_t)n * sizeof(vpcsum_nat_t));
+        if (dev_arena) {
+            // the frames live in a registered (page-locked, mapped) arena: rewritten where they lie
+            memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
+            if (n && nat_run(dev_arena - lo, arena_len, s.dh_desc, s.dh_rw, 1, n, s.dh_status, nat_mode, s.stream) != 0)
+                return -1;
+            s.zero_copy = true;
+        } else {
+            // staged: each packet's 16-B blocks gathered into the pinned staging, rewritten on the
+            // device, and the whole gathered batch copied back (the headers return at wait)
             uint64_t pos = 0;
             for (uint32_t i = 0; i < n; ++i) {
                 const vpcsum_desc_t& d = h_desc[i];
@@ -776,352 +1100,114 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
                 if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) { s.h_desc[i].l3_off = UINT64_MAX; continue; }
                 const uint64_t a0 = d.l3_off & ~(uint64_t)15;
                 const uint64_t a1 = std::min<uint64_t>((d.l3_off + d.l3_len + 15) & ~(uint64_t)15, arena_len);
-                if (pos + (a1 - a0) > c->max_arena) return fail("vpcsum_ctx_submit: gathered batch exceeds capacity");
+                if (pos + (a1 - a0) > c->max_arena) return fail("vpcsum_ctx_nat_submit: batch exceeds the staging capacity");
                 memcpy(s.h_arena + pos, h_arena + a0, a1 - a0);
                 s.h_desc[i].l3_off = pos + (d.l3_off - a0);
                 pos += (a1 - a0 + 15) & ~(uint64_t)15;
             }
-            dev_len = pos;
-        } else {
-            if (span > c->max_arena) return fail("vpcsum_ctx_submit: batch spans %llu bytes > capacity %llu",
-                                                 (unsigned long long)span, (unsigned long long)c->max_arena);
-            // descriptors rebased to the device copy of [lo, hi)
-            for (uint32_t i = 0; i < n; ++i) {
-                s.h_desc[i] = h_desc[i];
-                if (h_desc[i].l3_off >= lo) s.h_desc[i].l3_off = h_desc[i].l3_off - lo;
-                else s.h_desc[i].l3_off = UINT64_MAX;   // out of span -> BAD in the kernel
+            if (n) {
+                VPC_CHECK(hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)n * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice, s.stream),
+                          "H2D descriptors");
+                VPC_CHECK(hipMemcpyAsync(s.d_rw, s.h_rw, (size_t)n * sizeof(vpcsum_nat_t), hipMemcpyHostToDevice, s.stream),
+                          "H2D rewrites");
+                if (pos) VPC_CHECK(hipMemcpyAsync(s.d_arena, s.h_arena, pos, hipMemcpyHostToDevice, s.stream), "H2D frames");
+                if (nat_run(s.d_arena, pos, s.d_desc, s.d_rw, 1, n, s.d_status, nat_mode, s.stream) != 0) return -1;
+                if (pos) VPC_CHECK(hipMemcpyAsync(s.h_arena, s.d_arena, pos, hipMemcpyDeviceToHost, s.stream), "D2H frames");
+                VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
             }
+            s.zero_copy = false;
         }
-        VPC_CHECK(hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)n * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice, s.stream),
-                  "H2D descriptors");
-        if (dev_len) {
-            const uint8_t* src = gather ? s.h_arena : h_arena + lo;
-            if (!gather && !is_registered(c, src, span)) {
-                memcpy(s.h_arena, src, span);   // pageable -> pinned staging
-                src = s.h_arena;
-            }
-            VPC_CHECK(hipMemcpyAsync(s.d_arena, src, dev_len, hipMemcpyHostToDevice, s.stream), "H2D arena");
-        }
-        VPC_CHECK(launch_csum(s.d_arena, dev_len, s.d_desc, n, s.d_out, s.d_status, nullptr, mode & VPCSUM_MODE_VERIFY,
-                              nullptr, 0, 0, s.stream),
-                  "checksum launch");
-        VPC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream), "D2H out");
-        VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
-    }
-    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
-    s.kind = 0;
-    s.busy = true;
-    s.ticket = t;
-    s.n = n;
-    s.mode = mode;
-    s.user_arena = h_arena;
-    s.user_desc = h_desc;
-    s.user_out = h_out;
-    s.user_status = h_status;
-    *ticket = t;
-    return 0;
-}
-
-int vpcsum_ctx_wait(vpcsum_ctx_t* c, uint64_t ticket) {
-    if (!c) return fail("vpcsum_ctx_wait: NULL context");
-    std::lock_guard<std::mutex> lk(c->mu);
-    VPC_ON_DEVICE(c->device);
-    Slot& s = c->slots[ticket & 1];
-    if (!s.busy || s.ticket != ticket) {
-        if (ticket == 0 || ticket >= c->next_ticket) return fail("vpcsum_ctx_wait: unknown ticket %llu", (unsigned long long)ticket);
-        return 0;   // already completed
-    }
-    return slot_finish(c, s);
-}
-
-int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
-                             const uint32_t* h_frame_len, uint32_t n, uint32_t* h_out, uint8_t* h_status,
-                             uint64_t* ticket) {
-    if (!c || !ticket) return fail("vpcsum_ctx_verify_frames: NULL context or ticket");
-    if (n > c->max_pkts) return fail("vpcsum_ctx_verify_frames: %u frames > capacity %u", n, c->max_pkts);
-    if (n && (!h_arena || !h_frame_off || !h_frame_len || !h_status))
-        return fail("vpcsum_ctx_verify_frames: NULL arena, frame table or status");
-    std::lock_guard<std::mutex> lk(c->mu);
-    VPC_ON_DEVICE(c->device);
-    uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
-    if (n && !base) return fail("vpcsum_ctx_verify_frames: the arena must be registered (vpcsum_ctx_register_arena)");
-    const uint64_t t = c->next_ticket++;
-    Slot& s = c->slots[t & 1];
-    if (s.busy && slot_finish(c, s) != 0) return -1;
-    if (n) {
-        // parse the frames where they lie (zero-copy), then verify the descriptors it built
-        memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
-        memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
-        VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.d_desc,
-                                     nullptr, nullptr, s.stream),
-                  "parse launch");
-        VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, s.dh_out, s.dh_status, nullptr, VPCSUM_MODE_VERIFY, nullptr,
-                              n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
-                  "verify launch");
-    }
-    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
-    s.zero_copy = true;
-    s.svc_seq = 0;
-    s.kind = 0;
-    s.busy = true;
-    s.ticket = t;
-    s.n = n;
-    s.mode = VPCSUM_MODE_VERIFY;
-    s.user_arena = nullptr;
-    s.user_desc = nullptr;
-    s.user_out = h_out;
-    s.user_status = h_status;
-    *ticket = t;
-    return 0;
-}
-
-int vpcsum_ctx_egress_frames(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
-                             const uint32_t* h_frame_len, const uint8_t* h_frame_flags, uint32_t n, uint32_t* h_out,
-                             uint8_t* h_status, uint64_t* ticket) {
-    if (!c || !ticket) return fail("vpcsum_ctx_egress_frames: NULL context or ticket");
-    if (n > c->max_pkts) return fail("vpcsum_ctx_egress_frames: %u frames > capacity %u", n, c->max_pkts);
-    if (n && (!h_arena || !h_frame_off || !h_frame_len || !h_frame_flags))
-        return fail("vpcsum_ctx_egress_frames: NULL arena, frame table or flags");
-    std::lock_guard<std::mutex> lk(c->mu);
-    VPC_ON_DEVICE(c->device);
-    uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
-    if (n && !base) return fail("vpcsum_ctx_egress_frames: the arena must be registered (vpcsum_ctx_register_arena)");
-    const uint64_t t = c->next_ticket++;
-    Slot& s = c->slots[t & 1];
-    if (s.busy && slot_finish(c, s) != 0) return -1;
-    if (n) {
-        // the frames' own flags ride in the status staging: the parse reads them before the
-        // checksum kernel, later on the same stream, overwrites them with the statuses
-        memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
-        memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
-        memcpy(s.h_status, h_frame_flags, n);
-        VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, 0, s.d_desc, nullptr, nullptr, s.stream,
-                                     s.dh_status),
-                  "parse launch");
-        VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, s.dh_out, s.dh_status, nullptr, VPCSUM_MODE_COMPUTE, base,
-                              n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
-                  "checksum launch");
-    }
-    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
-    s.zero_copy = true;
-    s.svc_seq = 0;
-    s.kind = 0;
-    s.busy = true;
-    s.ticket = t;
-    s.n = n;
-    s.mode = VPCSUM_MODE_WRITE;
-    s.user_arena = nullptr;   // written in place through the mapping
-    s.user_desc = nullptr;
-    s.user_out = h_out;
-    s.user_status = h_status;
-    *ticket = t;
-    return 0;
-}
-
-int vpcsum_ctx_parse_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
-                            const uint32_t* h_frame_len, uint32_t n, vpcsum_desc_t* h_desc, uint8_t* h_status,
-                            vpcsum_tuple_t* h_tuples, uint64_t* ticket) {
-    if (!c || !ticket) return fail("vpcsum_ctx_parse_frames: NULL context or ticket");
-    if (n > c->max_pkts) return fail("vpcsum_ctx_parse_frames: %u frames > capacity %u", n, c->max_pkts);
-    if (n && (!h_arena || !h_frame_off || !h_frame_len)) return fail("vpcsum_ctx_parse_frames: NULL arena or frame table");
-    std::lock_guard<std::mutex> lk(c->mu);
-    VPC_ON_DEVICE(c->device);
-    uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
-    if (n && !base) return fail("vpcsum_ctx_parse_frames: the arena must be registered (vpcsum_ctx_register_arena)");
-    const uint64_t t = c->next_ticket++;
-    Slot& s = c->slots[t & 1];
-    if (s.busy && slot_finish(c, s) != 0) return -1;
-    if (!s.h_tu) {
-        hipError_t e = hipHostMalloc((void**)&s.h_tu, (size_t)c->max_pkts * sizeof(vpcsum_tuple_t),
-                                     hipHostMallocMapped | hipHostMallocCoherent);
-        if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s.dh_tu, s.h_tu, 0);
-        if (e != hipSuccess) {
-            if (s.h_tu) (void)hipHostFree(s.h_tu);
-            s.h_tu = s.dh_tu = nullptr;
-            return hipfail(e, "vpcsum_ctx_parse_frames allocation");
-        }
-    }
-    if (n) {
-        // parsed where the frames lie (zero-copy); results straight into the pinned staging
-        memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
-        memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
-        VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.dh_desc,
-                                     s.dh_status, s.dh_tu, s.stream),
-                  "parse launch");
-    }
-    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
-    s.zero_copy = true;
-    s.svc_seq = 0;
-    s.kind = 2;
-    s.busy = true;
-    s.ticket = t;
-    s.n = n;
-    s.mode = 0;
-    s.user_arena = nullptr;
-    s.user_desc = nullptr;
-    s.user_out = nullptr;
-    s.user_status = h_status;
-    s.user_desc_out = h_desc;
-    s.user_tuples = h_tuples;
-    *ticket = t;
-    return 0;
-}
-
-int vpcsum_ctx_nat_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
-                          const vpcsum_nat_t* h_rw, uint32_t n, uint8_t* h_status, uint32_t nat_mode, uint64_t* ticket) {
-    if (!c || !ticket) return fail("vpcsum_ctx_nat_submit: NULL context or ticket");
-    if (n > c->max_pkts) return fail("vpcsum_ctx_nat_submit: %u packets > capacity %u", n, c->max_pkts);
-    if (n && (!h_arena || !h_desc || !h_rw)) return fail("vpcsum_ctx_nat_submit: NULL arena, descriptors or rewrites");
-    if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u)) return fail("vpcsum_ctx_nat_submit: bad nat_mode 0x%x", nat_mode);
-    std::lock_guard<std::mutex> lk(c->mu);
-    VPC_ON_DEVICE(c->device);
-    const uint64_t t = c->next_ticket++;
-    Slot& s = c->slots[t & 1];
-    if (s.busy && slot_finish(c, s) != 0) return -1;
-    if (!s.h_rw) {
-        hipError_t e = hipSuccess;
-        const size_t bytes = (size_t)c->max_pkts * sizeof(vpcsum_nat_t);
-        if ((e = hipHostMalloc((void**)&s.h_rw, bytes, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
-            (e = hipHostGetDevicePointer((void**)&s.dh_rw, s.h_rw, 0)) != hipSuccess ||
-            (e = hipMalloc((void**)&s.d_rw, bytes)) != hipSuccess) {
-            if (s.h_rw) (void)hipHostFree(s.h_rw);
-            if (s.d_rw) (void)hipFree(s.d_rw);
-            s.h_rw = s.dh_rw = s.d_rw = nullptr;
-            return hipfail(e, "vpcsum_ctx_nat_submit allocation");
-        }
-    }
-    uint64_t lo = UINT64_MAX, hi = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const vpcsum_desc_t& d = h_desc[i];
-        if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) continue;   // the kernel flags it BAD
-        lo = std::min(lo, d.l3_off);
-        hi = std::max(hi, d.l3_off + d.l3_len);
-    }
-    if (lo == UINT64_MAX) { lo = 0; hi = 0; }
-    lo &= ~(uint64_t)15;
-    uint8_t* dev_arena = hi > lo ? mapped_dev(c, h_arena + lo, hi - lo) : nullptr;
-    memcpy(s.h_rw, h_rw, (size_t)n * sizeof(vpcsum_nat_t));
-    if (dev_arena) {
-        // the frames live in a registered (page-locked, mapped) arena: rewritten where they lie
-        memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
-        if (n && nat_run(dev_arena - lo, arena_len, s.dh_desc, s.dh_rw, 1, n, s.dh_status, nat_mode, s.stream) != 0)
-            return -1;
-        s.zero_copy = true;
-    } else {
-        // staged: each packet's 16-B blocks gathered into the pinned staging, rewritten on the
-        // device, and the whole gathered batch copied back (the headers return at wait)
-        uint64_t pos = 0;
-        for (uint32_t i = 0; i < n; ++i) {
-            const vpcsum_desc_t& d = h_desc[i];
-            s.h_desc[i] = d;
-            if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) { s.h_desc[i].l3_off = UINT64_MAX; continue; }
-            const uint64_t a0 = d.l3_off & ~(uint64_t)15;
-            const uint64_t a1 = std::min<uint64_t>((d.l3_off + d.l3_len + 15) & ~(uint64_t)15, arena_len);
-            if (pos + (a1 - a0) > c->max_arena) return fail("vpcsum_ctx_nat_submit: batch exceeds the staging capacity");
-            memcpy(s.h_arena + pos, h_arena + a0, a1 - a0);
-            s.h_desc[i].l3_off = pos + (d.l3_off - a0);
-            pos += (a1 - a0 + 15) & ~(uint64_t)15;
-        }
-        if (n) {
-            VPC_CHECK(hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)n * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice, s.stream),
-                      "H2D descriptors");
-            VPC_CHECK(hipMemcpyAsync(s.d_rw, s.h_rw, (size_t)n * sizeof(vpcsum_nat_t), hipMemcpyHostToDevice, s.stream),
-                      "H2D rewrites");
-            if (pos) VPC_CHECK(hipMemcpyAsync(s.d_arena, s.h_arena, pos, hipMemcpyHostToDevice, s.stream), "H2D frames");
-            if (nat_run(s.d_arena, pos, s.d_desc, s.d_rw, 1, n, s.d_status, nat_mode, s.stream) != 0) return -1;
-            if (pos) VPC_CHECK(hipMemcpyAsync(s.h_arena, s.d_arena, pos, hipMemcpyDeviceToHost, s.stream), "D2H frames");
-            VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
-        }
-        s.zero_copy = false;
-    }
-    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
-    s.kind = 1;
-    s.svc_seq = 0;
-    s.busy = true;
-    s.ticket = t;
-    s.n = n;
-    s.mode = nat_mode;
-    s.user_arena = h_arena;
-    s.user_desc = h_desc;
-    s.user_out = nullptr;
-    s.user_status = h_status;
-    *ticket = t;
-    return 0;
+        VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+        s.kind = 1;
+        s.svc_seq = 0;
+        s.busy = true;
+        s.ticket = t;
+        s.n = n;
+        s.mode = nat_mode;
+        s.user_arena = h_arena;
+        s.user_desc = h_desc;
+        s.user_out = nullptr;
+        s.user_status = h_status;
+        *ticket = t;
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_nat_submit")
 }
 
 int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint32_t copy_bytes,
                         const vpcsum_desc_t* h_desc, uint32_t n, uint32_t* h_out, uint32_t mode, uint32_t chunks) {
-    if (!c || !h_arena || !h_desc || !h_out) return fail("vpcsum_ctx_pipeline: NULL argument");
-    if (chunks == 0) chunks = 1;
-    if (copy_bytes > stride) return fail("vpcsum_ctx_pipeline: copy_bytes > stride");
-    if (mode & ~(VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_ctx_pipeline: bad mode");
-    std::lock_guard<std::mutex> lk(c->mu);
-    VPC_ON_DEVICE(c->device);
-    for (auto& s : c->slots)
-        if (s.busy && slot_finish(c, s) != 0) return -1;
-    const uint32_t per = (n + chunks - 1) / chunks;
-    if (per > c->max_pkts || (uint64_t)per * stride > c->max_arena)
-        return fail("vpcsum_ctx_pipeline: chunk of %u frames exceeds context capacity", per);
-    const bool pinned = is_registered(c, h_arena, (uint64_t)n * stride);
-    if (!pinned) return fail("vpcsum_ctx_pipeline: host arena must be registered (vpcsum_ctx_register_arena)");
-    // MODE_WRITE: the kernels read the device copy and store the checksum fields straight into the
-    // host frames through the registered arena's mapping (2-B posted PCIe writes), so the frames
-    // need no copy back
-    uint8_t* w = nullptr;
-    if (mode & VPCSUM_MODE_WRITE) {
-        w = mapped_dev(c, h_arena, (uint64_t)n * stride);
-        if (!w) return fail("vpcsum_ctx_pipeline: MODE_WRITE needs the arena registered with this context");
-    }
-    const bool desc_pinned = is_registered(c, (const uint8_t*)h_desc, (uint64_t)n * sizeof(vpcsum_desc_t));
-    const bool out_pinned = is_registered(c, (const uint8_t*)h_out, (uint64_t)n * 4);
-    if (!desc_pinned || !out_pinned) return fail("vpcsum_ctx_pipeline: descriptors and out must be registered");
-    // each chunk's device view starts at frame i0, and only the first copy_bytes of every frame
-    // are copied: a descriptor must lie inside the copied part of a frame of its own chunk
-    // (below the view it would address memory before the device slot)
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint64_t i0 = (uint64_t)(i / per) * per;
-        const uint64_t off = h_desc[i].l3_off;
-        if (off < i0 * stride || off >= (uint64_t)n * stride || off % stride + h_desc[i].l3_len > copy_bytes)
-            return fail("vpcsum_ctx_pipeline: descriptor %u [%llu, +%u) outside the copied frames", i,
-                        (unsigned long long)off, (unsigned)h_desc[i].l3_len);
-    }
-    // a failure after some chunks were queued drains both streams before it returns: the queued
-    // copies and in-place writes land in the caller's registered buffers
-#define VPC_CHECK_DRAIN(expr, what)                                                  \
-    do {                                                                             \
-        hipError_t e__ = (expr);                                                     \
-        if (e__ != hipSuccess) {                                                     \
-            const int rc__ = hipfail(e__, what);                                     \
-            for (auto& q__ : c->slots) (void)hipStreamSynchronize(q__.stream);       \
-            return rc__;                                                             \
-        }                                                                            \
-    } while (0)
-    for (uint32_t k = 0; k < chunks; ++k) {
-        const uint32_t i0 = k * per;
-        if (i0 >= n) break;
-        const uint32_t m = std::min(per, n - i0);
-        Slot& s = c->slots[k & 1];
-        // descriptors of this chunk address the device slot as frame (i - i0) * stride: the
-        // caller's descriptors are relative to frame i0 once i0 * stride is subtracted
-        VPC_CHECK_DRAIN(hipMemcpyAsync(s.d_desc, h_desc + i0, (size_t)m * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice,
-                                 s.stream),
-                  "pipeline H2D desc");
-        VPC_CHECK_DRAIN(hipMemcpy2DAsync(s.d_arena, stride, h_arena + (uint64_t)i0 * stride, stride, copy_bytes, m,
-                                   hipMemcpyHostToDevice, s.stream),
-                  "pipeline H2D frames");
-        VPC_CHECK_DRAIN(launch_csum(s.d_arena - (uint64_t)i0 * stride, (uint64_t)(i0 + m) * stride, s.d_desc, m, s.d_out,
-                              nullptr, nullptr, mode & VPCSUM_MODE_VERIFY, w, 0, 0, s.stream),
-                  "pipeline launch");
-        VPC_CHECK_DRAIN(hipMemcpyAsync(h_out + i0, s.d_out, (size_t)m * 4, hipMemcpyDeviceToHost, s.stream), "pipeline D2H");
-    }
-#undef VPC_CHECK_DRAIN
-    hipError_t es = hipSuccess;   // both streams are joined, the first error is reported
-    for (auto& s : c->slots) {
-        const hipError_t e2 = hipStreamSynchronize(s.stream);
-        if (es == hipSuccess) es = e2;
-    }
-    VPC_CHECK(es, "pipeline sync");
-    return 0;
+    try {
+        if (!c || !h_arena || !h_desc || !h_out) return fail("vpcsum_ctx_pipeline: NULL argument");
+        if (chunks == 0) chunks = 1;
+        if (copy_bytes > stride) return fail("vpcsum_ctx_pipeline: copy_bytes > stride");
+        if (mode & ~(VPCSUM_MODE_VERIFY | VPCSUM_MODE_WRITE)) return fail("vpcsum_ctx_pipeline: bad mode");
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        for (auto& s : c->slots)
+            if (s.busy && slot_finish(c, s) != 0) return -1;
+        const uint32_t per = (n + chunks - 1) / chunks;
+        if (per > c->max_pkts || (uint64_t)per * stride > c->max_arena)
+            return fail("vpcsum_ctx_pipeline: chunk of %u frames exceeds context capacity", per);
+        const bool pinned = is_registered(c, h_arena, (uint64_t)n * stride);
+        if (!pinned) return fail("vpcsum_ctx_pipeline: host arena must be registered (vpcsum_ctx_register_arena)");
+        // MODE_WRITE: the kernels read the device copy and store the checksum fields straight into the
+        // host frames through the registered arena's mapping (2-B posted PCIe writes), so the frames
+        // need no copy back
+        uint8_t* w = nullptr;
+        if (mode & VPCSUM_MODE_WRITE) {
+            w = mapped_dev(c, h_arena, (uint64_t)n * stride);
+            if (!w) return fail("vpcsum_ctx_pipeline: MODE_WRITE needs the arena registered with this context");
+        }
+        const bool desc_pinned = is_registered(c, (const uint8_t*)h_desc, (uint64_t)n * sizeof(vpcsum_desc_t));
+        const bool out_pinned = is_registered(c, (const uint8_t*)h_out, (uint64_t)n * 4);
+        if (!desc_pinned || !out_pinned) return fail("vpcsum_ctx_pipeline: descriptors and out must be registered");
+        // each chunk's device view starts at frame i0, and only the first copy_bytes of every frame
+        // are copied: a descriptor must lie inside the copied part of a frame of its own chunk
+        // (below the view it would address memory before the device slot)
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint64_t i0 = (uint64_t)(i / per) * per;
+            const uint64_t off = h_desc[i].l3_off;
+            if (off < i0 * stride || off >= (uint64_t)n * stride || off % stride + h_desc[i].l3_len > copy_bytes)
+                return fail("vpcsum_ctx_pipeline: descriptor %u [%llu, +%u) outside the copied frames", i,
+                            (unsigned long long)off, (unsigned)h_desc[i].l3_len);
+        }
+        // a failure after some chunks were queued drains both streams before it returns: the queued
+        // copies and in-place writes land in the caller's registered buffers
+    #define VPC_CHECK_DRAIN(expr, what)                                                  \
+        do {                                                                             \
+            hipError_t e__ = (expr);                                                     \
+            if (e__ != hipSuccess) {                                                     \
+                const int rc__ = hipfail(e__, what);                                     \
+                for (auto& q__ : c->slots) (void)hipStreamSynchronize(q__.stream);       \
+                return rc__;                                                             \
+            }                                                                            \
+        } while (0)
+        for (uint32_t k = 0; k < chunks; ++k) {
+            const uint32_t i0 = k * per;
+            if (i0 >= n) break;
+            const uint32_t m = std::min(per, n - i0);
+            Slot& s = c->slots[k & 1];
+            // descriptors of this chunk address the device slot as frame (i - i0) * stride: the
+            // caller's descriptors are relative to frame i0 once i0 * stride is subtracted
+            VPC_CHECK_DRAIN(hipMemcpyAsync(s.d_desc, h_desc + i0, (size_t)m * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice,
+                                     s.stream),
+                      "pipeline H2D desc");
+            VPC_CHECK_DRAIN(hipMemcpy2DAsync(s.d_arena, stride, h_arena + (uint64_t)i0 * stride, stride, copy_bytes, m,
+                                       hipMemcpyHostToDevice, s.stream),
+                      "pipeline H2D frames");
+            VPC_CHECK_DRAIN(launch_csum(s.d_arena - (uint64_t)i0 * stride, (uint64_t)(i0 + m) * stride, s.d_desc, m, s.d_out,
+                                  nullptr, nullptr, mode & VPCSUM_MODE_VERIFY, w, 0, 0, s.stream),
+                      "pipeline launch");
+            VPC_CHECK_DRAIN(hipMemcpyAsync(h_out + i0, s.d_out, (size_t)m * 4, hipMemcpyDeviceToHost, s.stream), "pipeline D2H");
+        }
+    #undef VPC_CHECK_DRAIN
+        hipError_t es = hipSuccess;   // both streams are joined, the first error is reported
+        for (auto& s : c->slots) {
+            const hipError_t e2 = hipStreamSynchronize(s.stream);
+            if (es == hipSuccess) es = e2;
+        }
+        VPC_CHECK(es, "pipeline sync");
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_pipeline")
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1152,86 +1238,114 @@ extern "C" {
 
 int vpcsum_group_create_list(const int* devices, int ndev, uint64_t max_arena_bytes, uint32_t max_pkts,
                              vpcsum_group_t** out) {
-    if (!out || !devices || ndev <= 0 || ndev > 64) return fail("vpcsum_group_create_list: bad argument");
-    vpcsum_group* g = new vpcsum_group();
-    for (int i = 0; i < ndev; ++i) {
-        vpcsum_ctx_t* c = nullptr;
-        if (vpcsum_ctx_create(devices[i], max_arena_bytes, max_pkts, &c) != 0) {
-            const std::string e = g_err;
-            vpcsum_group_destroy(g);
-            return fail("%s", e.c_str());
+    try {
+        if (!out || !devices || ndev <= 0 || ndev > 64) return fail("vpcsum_group_create_list: bad argument");
+        std::unique_ptr<vpcsum_group> g(new vpcsum_group());
+        g->ctx.reserve(ndev);   // the push_backs below cannot throw once a context exists
+        for (int i = 0; i < ndev; ++i) {
+            vpcsum_ctx_t* c = nullptr;
+            if (vpcsum_ctx_create(devices[i], max_arena_bytes, max_pkts, &c) != 0) {
+                char e[1024];
+                snprintf(e, sizeof(e), "%s", g_err);
+                vpcsum_group_destroy(g.release());
+                return fail("%s", e);
+            }
+            g->ctx.push_back(c);
         }
-        g->ctx.push_back(c);
-    }
-    *out = g;
-    return 0;
+        *out = g.release();
+        return 0;
+    } VPC_CATCH("vpcsum_group_create_list")
 }
 
 int vpcsum_group_create(uint64_t dev_mask, uint64_t max_arena_bytes, uint32_t max_pkts, vpcsum_group_t** out) {
-    int n = 0;
-    VPC_CHECK(hipGetDeviceCount(&n), "hipGetDeviceCount");
-    std::vector<int> devs;
-    for (int d = 0; d < 64 && d < n; ++d)
-        if (dev_mask >> d & 1) devs.push_back(d);
-    if (devs.empty() || (n < 64 && (dev_mask >> n) != 0))
-        return fail("vpcsum_group_create: mask 0x%llx names no device or one beyond the %d present",
-                    (unsigned long long)dev_mask, n);
-    return vpcsum_group_create_list(devs.data(), (int)devs.size(), max_arena_bytes, max_pkts, out);
+    try {
+        int n = 0;
+        VPC_CHECK(hipGetDeviceCount(&n), "hipGetDeviceCount");
+        std::vector<int> devs;
+        for (int d = 0; d < 64 && d < n; ++d)
+            if (dev_mask >> d & 1) devs.push_back(d);
+        if (devs.empty() || (n < 64 && (dev_mask >> n) != 0))
+            return fail("vpcsum_group_create: mask 0x%llx names no device or one beyond the %d present",
+                        (unsigned long long)dev_mask, n);
+        return vpcsum_group_create_list(devs.data(), (int)devs.size(), max_arena_bytes, max_pkts, out);
+    } VPC_CATCH("vpcsum_group_create")
 }
 
 int vpcsum_group_destroy(vpcsum_group_t* g) {
-    if (!g) return 0;
-    for (auto* c : g->ctx) vpcsum_ctx_destroy(c);
-    for (auto* h : g->reg) (void)hipHostUnregister(h);
-    delete g;
-    return 0;
+    try {
+        if (!g) return 0;
+        for (auto* c : g->ctx) vpcsum_ctx_destroy(c);
+        for (auto* h : g->reg) (void)hipHostUnregister(h);
+        delete g;
+        return 0;
+    } VPC_CATCH("vpcsum_group_destroy")
 }
 
 int vpcsum_group_register_arena(vpcsum_group_t* g, void* h_arena, uint64_t len) {
-    if (!g || !h_arena || len == 0) return fail("vpcsum_group_register_arena: bad argument");
-    std::lock_guard<std::mutex> lk(g->mu);
-    VPC_ON_DEVICE(g->ctx[0]->device);
-    VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterMapped | hipHostRegisterPortable), "hipHostRegister");
-    for (size_t i = 0; i < g->ctx.size(); ++i) {
-        vpcsum_ctx* c = g->ctx[i];
-        std::lock_guard<std::mutex> lc(c->mu);
-        DeviceScope on_dev(c->device);
-        void* dev = nullptr;
-        hipError_t e = on_dev.err;
-        if (e == hipSuccess) e = hipHostGetDevicePointer(&dev, h_arena, 0);
-        if (e != hipSuccess) {
-            // roll back: no context keeps a mapping of an arena the group failed to register, so
-            // a retry starts from scratch
-            for (size_t q = 0; q < i; ++q) {
-                std::lock_guard<std::mutex> lq(g->ctx[q]->mu);
-                auto& rq = g->ctx[q]->registered;
-                for (size_t k = rq.size(); k-- > 0;)
-                    if (rq[k].host == (uint8_t*)h_arena && !rq[k].owned) rq.erase(rq.begin() + k);
-            }
-            (void)hipHostUnregister(h_arena);
-            return hipfail(e, "vpcsum_group_register_arena: device mapping");
+    try {
+        if (!g || !h_arena || len == 0) return fail("vpcsum_group_register_arena: bad argument");
+        std::lock_guard<std::mutex> lk(g->mu);
+        VPC_ON_DEVICE(g->ctx[0]->device);
+        // the bookkeeping may throw: make room before anything is pinned or mapped
+        g->reg.reserve(g->reg.size() + 1);
+        for (auto* c : g->ctx) {
+            std::lock_guard<std::mutex> lc(c->mu);
+            c->registered.reserve(c->registered.size() + 1);
         }
-        c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, false});
-    }
-    g->reg.push_back((uint8_t*)h_arena);
-    return 0;
+        VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterMapped | hipHostRegisterPortable), "hipHostRegister");
+        for (size_t i = 0; i < g->ctx.size(); ++i) {
+            vpcsum_ctx* c = g->ctx[i];
+            std::lock_guard<std::mutex> lc(c->mu);
+            DeviceScope on_dev(c->device);
+            void* dev = nullptr;
+            hipError_t e = on_dev.err;
+            if (e == hipSuccess) e = hipHostGetDevicePointer(&dev, h_arena, 0);
+            if (e != hipSuccess) {
+                // roll back: no context keeps a mapping of an arena the group failed to register, so
+                // a retry starts from scratch
+                for (size_t q = 0; q < i; ++q) {
+                    std::lock_guard<std::mutex> lq(g->ctx[q]->mu);
+                    auto& rq = g->ctx[q]->registered;
+                    for (size_t k = rq.size(); k-- > 0;)
+                        if (rq[k].host == (uint8_t*)h_arena && !rq[k].owned) rq.erase(rq.begin() + k);
+                }
+                (void)hipHostUnregister(h_arena);
+                return hipfail(e, "vpcsum_group_register_arena: device mapping");
+            }
+            c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, false});
+        }
+        g->reg.push_back((uint8_t*)h_arena);
+        return 0;
+    } VPC_CATCH("vpcsum_group_register_arena")
 }
 
 int vpcsum_group_unregister_arena(vpcsum_group_t* g, void* h_arena) {
-    if (!g || !h_arena) return fail("vpcsum_group_unregister_arena: bad argument");
-    std::lock_guard<std::mutex> lk(g->mu);
-    auto it = std::find(g->reg.begin(), g->reg.end(), (uint8_t*)h_arena);
-    if (it == g->reg.end()) return fail("vpcsum_group_unregister_arena: arena not registered");
-    // every context finishes its zero-copy batches on the arena and forgets the mapping
-    // (vpcsum_ctx_unregister_arena; the contexts do not own the page-lock), then the group unpins it
-    int rc = 0;
-    for (auto* c : g->ctx)
-        if (vpcsum_ctx_unregister_arena(c, h_arena) != 0) rc = -1;
-    if (rc != 0) return -1;
-    g->reg.erase(it);
-    VPC_ON_DEVICE(g->ctx[0]->device);
-    VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
-    return 0;
+    try {
+        if (!g || !h_arena) return fail("vpcsum_group_unregister_arena: bad argument");
+        std::lock_guard<std::mutex> lk(g->mu);
+        auto it = std::find(g->reg.begin(), g->reg.end(), (uint8_t*)h_arena);
+        if (it == g->reg.end()) return fail("vpcsum_group_unregister_arena: arena not registered");
+        // Two phases, so that a failure leaves the registration whole and a retry can succeed:
+        // (1) every context finishes its zero-copy batches -- the only step that can fail, and
+        // nothing has been dropped yet; (2) every context forgets the mapping (the contexts do not own
+        // the page-lock) and the group unpins the arena.
+        for (auto* c : g->ctx) {
+            std::lock_guard<std::mutex> lc(c->mu);
+            DeviceScope on_dev(c->device);
+            if (on_dev.err != hipSuccess) return hipfail(on_dev.err, "hipSetDevice");
+            if (ctx_quiesce_zero_copy(c) != 0) return -1;
+        }
+        for (auto* c : g->ctx) {
+            std::lock_guard<std::mutex> lc(c->mu);
+            auto& r = c->registered;
+            for (size_t k = r.size(); k-- > 0;)
+                if (r[k].host == (uint8_t*)h_arena && !r[k].owned) r.erase(r.begin() + k);
+        }
+        g->reg.erase(it);
+        VPC_ON_DEVICE(g->ctx[0]->device);
+        VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
+        return 0;
+    } VPC_CATCH("vpcsum_group_unregister_arena")
 }
 
 }  // extern "C"
@@ -1261,10 +1375,11 @@ static int group_submit_ranges(vpcsum_group* g, const vpcsum_desc_t* h_desc, uin
     for (size_t d = 0; d < k; ++d) {
         const uint32_t a = cut[d], b = std::max(cut[d], cut[d + 1]);
         if (submit(d, a, b, &slot.sub[d]) != 0) {
-            const std::string e = g_err;
+            char e[1024];
+            snprintf(e, sizeof(e), "%s", g_err);
             for (size_t q = 0; q < d; ++q) (void)vpcsum_ctx_wait(g->ctx[q], slot.sub[q]);
             slot.sub.clear();
-            return fail("%s", e.c_str());
+            return fail("%s", e);
         }
     }
     slot.ticket = t;
@@ -1276,218 +1391,265 @@ extern "C" {
 
 int vpcsum_group_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
                         uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket) {
-    if (!g || !ticket) return fail("vpcsum_group_submit: NULL group or ticket");
-    if (n && (!h_arena || !h_desc)) return fail("vpcsum_group_submit: NULL arena or descriptors");
-    std::lock_guard<std::mutex> lk(g->mu);
-    return group_submit_ranges(g, h_desc, n, ticket, [&](size_t d, uint32_t a, uint32_t b, uint64_t* t) {
-        return vpcsum_ctx_submit(g->ctx[d], h_arena, arena_len, h_desc + a, b - a, h_out ? h_out + a : nullptr,
-                                 h_status ? h_status + a : nullptr, mode, t);
-    });
+    try {
+        if (!g || !ticket) return fail("vpcsum_group_submit: NULL group or ticket");
+        if (n && (!h_arena || !h_desc)) return fail("vpcsum_group_submit: NULL arena or descriptors");
+        std::lock_guard<std::mutex> lk(g->mu);
+        return group_submit_ranges(g, h_desc, n, ticket, [&](size_t d, uint32_t a, uint32_t b, uint64_t* t) {
+            return vpcsum_ctx_submit(g->ctx[d], h_arena, arena_len, h_desc + a, b - a, h_out ? h_out + a : nullptr,
+                                     h_status ? h_status + a : nullptr, mode, t);
+        });
+    } VPC_CATCH("vpcsum_group_submit")
 }
 
 int vpcsum_group_nat_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
                             const vpcsum_nat_t* h_rw, uint32_t n, uint8_t* h_status, uint32_t nat_mode,
                             uint64_t* ticket) {
-    if (!g || !ticket) return fail("vpcsum_group_nat_submit: NULL group or ticket");
-    if (n && (!h_arena || !h_desc || !h_rw)) return fail("vpcsum_group_nat_submit: NULL arena, descriptors or rewrites");
-    std::lock_guard<std::mutex> lk(g->mu);
-    return group_submit_ranges(g, h_desc, n, ticket, [&](size_t d, uint32_t a, uint32_t b, uint64_t* t) {
-        return vpcsum_ctx_nat_submit(g->ctx[d], h_arena, arena_len, h_desc + a, h_rw + a, b - a,
-                                     h_status ? h_status + a : nullptr, nat_mode, t);
-    });
+    try {
+        if (!g || !ticket) return fail("vpcsum_group_nat_submit: NULL group or ticket");
+        if (n && (!h_arena || !h_desc || !h_rw)) return fail("vpcsum_group_nat_submit: NULL arena, descriptors or rewrites");
+        std::lock_guard<std::mutex> lk(g->mu);
+        return group_submit_ranges(g, h_desc, n, ticket, [&](size_t d, uint32_t a, uint32_t b, uint64_t* t) {
+            return vpcsum_ctx_nat_submit(g->ctx[d], h_arena, arena_len, h_desc + a, h_rw + a, b - a,
+                                         h_status ? h_status + a : nullptr, nat_mode, t);
+        });
+    } VPC_CATCH("vpcsum_group_nat_submit")
 }
 
 int vpcsum_group_wait(vpcsum_group_t* g, uint64_t ticket) {
-    if (!g) return fail("vpcsum_group_wait: NULL group");
-    std::lock_guard<std::mutex> lk(g->mu);
-    auto& slot = g->slots[ticket & 1];
-    if (slot.ticket != ticket) {
-        if (ticket == 0 || ticket >= g->next_ticket) return fail("vpcsum_group_wait: unknown ticket %llu", (unsigned long long)ticket);
-        return 0;   // already completed
-    }
-    return vpcsum_group_wait_locked(g, slot);
+    try {
+        if (!g) return fail("vpcsum_group_wait: NULL group");
+        std::lock_guard<std::mutex> lk(g->mu);
+        auto& slot = g->slots[ticket & 1];
+        if (slot.ticket != ticket) {
+            if (ticket == 0 || ticket >= g->next_ticket) return fail("vpcsum_group_wait: unknown ticket %llu", (unsigned long long)ticket);
+            return 0;   // already completed
+        }
+        return vpcsum_group_wait_locked(g, slot);
+    } VPC_CATCH("vpcsum_group_wait")
 }
 
 // SURVEY.md §8(b)'s entry points over one process-wide device group (vpcsum_init creates it).
-// vpcsum_shutdown must not race a submit or wait of another thread: the caller quiesces first,
-// as with vpcsum_group_destroy.
-static std::mutex g_default_mu;
+// Every call on the group holds a shared lock for its whole duration and vpcsum_init /
+// vpcsum_shutdown an exclusive one: a shutdown on one thread waits for the submits and waits in
+// flight on others, and a call after it fails with "vpcsum_init first" (never a freed group).
+}  // extern "C"
+
+static std::shared_mutex g_default_rw;
 static vpcsum_group* g_default = nullptr;
 
-static vpcsum_group* default_group(const char* what) {
-    std::lock_guard<std::mutex> lk(g_default_mu);
-    if (!g_default) fail("%s: vpcsum_init first", what);
-    return g_default;
+template <class F>
+static int with_default_group(const char* what, F f) {
+    std::shared_lock<std::shared_mutex> lk(g_default_rw);
+    if (!g_default) return fail("%s: vpcsum_init first", what);
+    return f(g_default);
 }
 
+extern "C" {
+
 int vpcsum_init(uint64_t dev_mask, uint64_t max_arena_bytes, uint32_t max_pkts) {
-    std::lock_guard<std::mutex> lk(g_default_mu);
-    if (g_default) return fail("vpcsum_init: already initialised (vpcsum_shutdown first)");
-    vpcsum_group_t* g = nullptr;
-    if (vpcsum_group_create(dev_mask, max_arena_bytes, max_pkts, &g) != 0) return -1;
-    g_default = g;
-    return 0;
+    try {
+        std::unique_lock<std::shared_mutex> lk(g_default_rw);
+        if (g_default) return fail("vpcsum_init: already initialised (vpcsum_shutdown first)");
+        vpcsum_group_t* g = nullptr;
+        if (vpcsum_group_create(dev_mask, max_arena_bytes, max_pkts, &g) != 0) return -1;
+        g_default = g;
+        return 0;
+    } VPC_CATCH("vpcsum_init")
 }
 
 int vpcsum_shutdown(void) {
-    std::lock_guard<std::mutex> lk(g_default_mu);
-    vpcsum_group_t* g = g_default;
-    g_default = nullptr;
-    return vpcsum_group_destroy(g);
+    try {
+        std::unique_lock<std::shared_mutex> lk(g_default_rw);
+        vpcsum_group_t* g = g_default;
+        g_default = nullptr;
+        return vpcsum_group_destroy(g);
+    } VPC_CATCH("vpcsum_shutdown")
 }
 
 int vpcsum_register_arena(void* h_arena, uint64_t len) {
-    vpcsum_group* g = default_group("vpcsum_register_arena");
-    return g ? vpcsum_group_register_arena(g, h_arena, len) : -1;
+    try {
+        return with_default_group("vpcsum_register_arena",
+                                  [&](vpcsum_group* g) { return vpcsum_group_register_arena(g, h_arena, len); });
+    } VPC_CATCH("vpcsum_register_arena")
 }
 
 int vpcsum_batch_submit(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, uint32_t n,
                         uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* handle) {
-    vpcsum_group* g = default_group("vpcsum_batch_submit");
-    return g ? vpcsum_group_submit(g, h_arena, arena_len, h_desc, n, h_out, h_status, mode, handle) : -1;
+    try {
+        return with_default_group("vpcsum_batch_submit", [&](vpcsum_group* g) {
+            return vpcsum_group_submit(g, h_arena, arena_len, h_desc, n, h_out, h_status, mode, handle);
+        });
+    } VPC_CATCH("vpcsum_batch_submit")
 }
 
 int vpcsum_nat_submit(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, const vpcsum_nat_t* h_rw,
                       uint32_t n, uint8_t* h_status, uint32_t nat_mode, uint64_t* handle) {
-    vpcsum_group* g = default_group("vpcsum_nat_submit");
-    return g ? vpcsum_group_nat_submit(g, h_arena, arena_len, h_desc, h_rw, n, h_status, nat_mode, handle) : -1;
+    try {
+        return with_default_group("vpcsum_nat_submit", [&](vpcsum_group* g) {
+            return vpcsum_group_nat_submit(g, h_arena, arena_len, h_desc, h_rw, n, h_status, nat_mode, handle);
+        });
+    } VPC_CATCH("vpcsum_nat_submit")
 }
 
 int vpcsum_batch_wait(uint64_t handle) {
-    vpcsum_group* g = default_group("vpcsum_batch_wait");
-    return g ? vpcsum_group_wait(g, handle) : -1;
+    try {
+        return with_default_group("vpcsum_batch_wait", [&](vpcsum_group* g) { return vpcsum_group_wait(g, handle); });
+    } VPC_CATCH("vpcsum_batch_wait")
 }
 
 // ------------------------------------------------------------------------------------------
 // PNI entry points
 // ------------------------------------------------------------------------------------------
 // The exception travels in env->ex as PNIThrowException stores it (pni.h:74-80); errno_ carries
-// EINVAL for argument errors and EIO for failures of the device runtime (PNIStoreErrno's slot,
-// pni.h:86-89), so Java code that inspects it sees a meaningful value.
+// EINVAL for argument errors, ENOMEM when host memory ran out and EIO for failures of the device
+// runtime (PNIStoreErrno's slot, pni.h:86-89), so Java code that inspects it sees a meaningful value.
 static int pni_throw(void* env, const char* type) {
     PNIException_vpcsum* ex = (PNIException_vpcsum*)env;
     ex->type = (char*)type;
-    strncpy(ex->message, g_err.c_str(), sizeof(ex->message));
+    strncpy(ex->message, g_err, sizeof(ex->message));
     ex->message[sizeof(ex->message) - 1] = '\0';
-    ex->errno_ = strcmp(type, "java.lang.IllegalArgumentException") == 0 ? EINVAL : EIO;
+    ex->errno_ = strcmp(type, "java.lang.IllegalArgumentException") == 0 ? EINVAL
+                 : strcmp(type, "java.lang.OutOfMemoryError") == 0       ? ENOMEM
+                                                                         : EIO;
     return -1;
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_create(PNIEnv_vpcsum_long* env, int32_t device, int64_t maxArena, int32_t maxPkts) {
-    if (maxArena <= 0 || maxPkts <= 0) {
-        fail("maxArena and maxPkts must be positive");
-        return pni_throw(env, "java.lang.IllegalArgumentException");
-    }
-    vpcsum_ctx_t* c = nullptr;
-    if (vpcsum_ctx_create(device, (uint64_t)maxArena, (uint32_t)maxPkts, &c) != 0) return pni_throw(env, "java.io.IOException");
-    env->return_ = (int64_t)(intptr_t)c;
-    return 0;
+    try {
+        if (maxArena <= 0 || maxPkts <= 0) {
+            fail("maxArena and maxPkts must be positive");
+            return pni_throw(env, "java.lang.IllegalArgumentException");
+        }
+        vpcsum_ctx_t* c = nullptr;
+        if (vpcsum_ctx_create(device, (uint64_t)maxArena, (uint32_t)maxPkts, &c) != 0) return pni_throw(env, "java.io.IOException");
+        env->return_ = (int64_t)(intptr_t)c;
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_create")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_registerArena(PNIEnv_vpcsum_void* env, int64_t ctx, void* arena, int64_t len) {
-    if (len <= 0) {
-        fail("len must be positive");
-        return pni_throw(env, "java.lang.IllegalArgumentException");
-    }
-    if (vpcsum_ctx_register_arena((vpcsum_ctx_t*)(intptr_t)ctx, arena, (uint64_t)len) != 0)
-        return pni_throw(env, "java.io.IOException");
-    return 0;
+    try {
+        if (len <= 0) {
+            fail("len must be positive");
+            return pni_throw(env, "java.lang.IllegalArgumentException");
+        }
+        if (vpcsum_ctx_register_arena((vpcsum_ctx_t*)(intptr_t)ctx, arena, (uint64_t)len) != 0)
+            return pni_throw(env, "java.io.IOException");
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_registerArena")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_submit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen, void* desc,
                                         int32_t n, void* out, void* status, int32_t mode) {
-    if (n < 0 || arenaLen < 0) {
-        fail("negative length");
-        return pni_throw(env, "java.lang.IllegalArgumentException");
-    }
-    uint64_t t = 0;
-    if (vpcsum_ctx_submit((vpcsum_ctx_t*)(intptr_t)ctx, (uint8_t*)arena, (uint64_t)arenaLen, (const vpcsum_desc_t*)desc,
-                          (uint32_t)n, (uint32_t*)out, (uint8_t*)status, (uint32_t)mode, &t) != 0)
-        return pni_throw(env, "java.io.IOException");
-    env->return_ = (int64_t)t;
-    return 0;
+    try {
+        if (n < 0 || arenaLen < 0) {
+            fail("negative length");
+            return pni_throw(env, "java.lang.IllegalArgumentException");
+        }
+        uint64_t t = 0;
+        if (vpcsum_ctx_submit((vpcsum_ctx_t*)(intptr_t)ctx, (uint8_t*)arena, (uint64_t)arenaLen, (const vpcsum_desc_t*)desc,
+                              (uint32_t)n, (uint32_t*)out, (uint8_t*)status, (uint32_t)mode, &t) != 0)
+            return pni_throw(env, "java.io.IOException");
+        env->return_ = (int64_t)t;
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_submit")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_waitFor(PNIEnv_vpcsum_void* env, int64_t ctx, int64_t ticket) {
-    if (vpcsum_ctx_wait((vpcsum_ctx_t*)(intptr_t)ctx, (uint64_t)ticket) != 0) return pni_throw(env, "java.io.IOException");
-    return 0;
+    try {
+        if (vpcsum_ctx_wait((vpcsum_ctx_t*)(intptr_t)ctx, (uint64_t)ticket) != 0) return pni_throw(env, "java.io.IOException");
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_waitFor")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                               void* frameOff, void* frameLen, int32_t n, void* out, void* status) {
-    if (n < 0 || arenaLen < 0) {
-        fail("verifyFrames: negative size");
-        return pni_throw(env, "java.lang.IllegalArgumentException");
-    }
-    uint64_t t = 0;
-    if (vpcsum_ctx_verify_frames((vpcsum_ctx_t*)(intptr_t)ctx, (const uint8_t*)arena, (uint64_t)arenaLen,
-                                 (const uint64_t*)frameOff, (const uint32_t*)frameLen, (uint32_t)n, (uint32_t*)out,
-                                 (uint8_t*)status, &t) != 0)
-        return pni_throw(env, "java.io.IOException");
-    env->return_ = (int64_t)t;
-    return 0;
+    try {
+        if (n < 0 || arenaLen < 0) {
+            fail("verifyFrames: negative size");
+            return pni_throw(env, "java.lang.IllegalArgumentException");
+        }
+        uint64_t t = 0;
+        if (vpcsum_ctx_verify_frames((vpcsum_ctx_t*)(intptr_t)ctx, (const uint8_t*)arena, (uint64_t)arenaLen,
+                                     (const uint64_t*)frameOff, (const uint32_t*)frameLen, (uint32_t)n, (uint32_t*)out,
+                                     (uint8_t*)status, &t) != 0)
+            return pni_throw(env, "java.io.IOException");
+        env->return_ = (int64_t)t;
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_verifyFrames")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_egressFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                               void* frameOff, void* frameLen, void* frameFlags, int32_t n, void* out,
                                               void* status) {
-    if (n < 0 || arenaLen < 0) {
-        fail("egressFrames: negative size");
-        return pni_throw(env, "java.lang.IllegalArgumentException");
-    }
-    uint64_t t = 0;
-    if (vpcsum_ctx_egress_frames((vpcsum_ctx_t*)(intptr_t)ctx, (uint8_t*)arena, (uint64_t)arenaLen,
-                                 (const uint64_t*)frameOff, (const uint32_t*)frameLen, (const uint8_t*)frameFlags,
-                                 (uint32_t)n, (uint32_t*)out, (uint8_t*)status, &t) != 0)
-        return pni_throw(env, "java.io.IOException");
-    env->return_ = (int64_t)t;
-    return 0;
+    try {
+        if (n < 0 || arenaLen < 0) {
+            fail("egressFrames: negative size");
+            return pni_throw(env, "java.lang.IllegalArgumentException");
+        }
+        uint64_t t = 0;
+        if (vpcsum_ctx_egress_frames((vpcsum_ctx_t*)(intptr_t)ctx, (uint8_t*)arena, (uint64_t)arenaLen,
+                                     (const uint64_t*)frameOff, (const uint32_t*)frameLen, (const uint8_t*)frameFlags,
+                                     (uint32_t)n, (uint32_t*)out, (uint8_t*)status, &t) != 0)
+            return pni_throw(env, "java.io.IOException");
+        env->return_ = (int64_t)t;
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_egressFrames")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_parseFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                              void* frameOff, void* frameLen, int32_t n, void* desc, void* status,
                                              void* tuples) {
-    if (n < 0 || arenaLen < 0) {
-        fail("parseFrames: negative size");
-        return pni_throw(env, "java.lang.IllegalArgumentException");
-    }
-    uint64_t t = 0;
-    if (vpcsum_ctx_parse_frames((vpcsum_ctx_t*)(intptr_t)ctx, (const uint8_t*)arena, (uint64_t)arenaLen,
-                                (const uint64_t*)frameOff, (const uint32_t*)frameLen, (uint32_t)n,
-                                (vpcsum_desc_t*)desc, (uint8_t*)status, (vpcsum_tuple_t*)tuples, &t) != 0)
-        return pni_throw(env, "java.io.IOException");
-    env->return_ = (int64_t)t;
-    return 0;
+    try {
+        if (n < 0 || arenaLen < 0) {
+            fail("parseFrames: negative size");
+            return pni_throw(env, "java.lang.IllegalArgumentException");
+        }
+        uint64_t t = 0;
+        if (vpcsum_ctx_parse_frames((vpcsum_ctx_t*)(intptr_t)ctx, (const uint8_t*)arena, (uint64_t)arenaLen,
+                                    (const uint64_t*)frameOff, (const uint32_t*)frameLen, (uint32_t)n,
+                                    (vpcsum_desc_t*)desc, (uint8_t*)status, (vpcsum_tuple_t*)tuples, &t) != 0)
+            return pni_throw(env, "java.io.IOException");
+        env->return_ = (int64_t)t;
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_parseFrames")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_natSubmit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                            void* desc, void* rw, int32_t n, void* status, int32_t natMode) {
-    if (n < 0 || arenaLen < 0) {
-        fail("natSubmit: negative size");
-        return pni_throw(env, "java.lang.IllegalArgumentException");
-    }
-    uint64_t t = 0;
-    if (vpcsum_ctx_nat_submit((vpcsum_ctx_t*)(intptr_t)ctx, (uint8_t*)arena, (uint64_t)arenaLen,
-                              (const vpcsum_desc_t*)desc, (const vpcsum_nat_t*)rw, (uint32_t)n, (uint8_t*)status,
-                              (uint32_t)natMode, &t) != 0)
-        return pni_throw(env, "java.io.IOException");
-    env->return_ = (int64_t)t;
-    return 0;
+    try {
+        if (n < 0 || arenaLen < 0) {
+            fail("natSubmit: negative size");
+            return pni_throw(env, "java.lang.IllegalArgumentException");
+        }
+        uint64_t t = 0;
+        if (vpcsum_ctx_nat_submit((vpcsum_ctx_t*)(intptr_t)ctx, (uint8_t*)arena, (uint64_t)arenaLen,
+                                  (const vpcsum_desc_t*)desc, (const vpcsum_nat_t*)rw, (uint32_t)n, (uint8_t*)status,
+                                  (uint32_t)natMode, &t) != 0)
+            return pni_throw(env, "java.io.IOException");
+        env->return_ = (int64_t)t;
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_natSubmit")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_setService(PNIEnv_vpcsum_void* env, int64_t ctx, int32_t idleUs) {
-    if (idleUs < 0) {
-        fail("setService: negative idle time %d", idleUs);
-        return pni_throw(env, "java.lang.IllegalArgumentException");
-    }
-    if (vpcsum_ctx_set_service((vpcsum_ctx_t*)(intptr_t)ctx, (uint32_t)idleUs) != 0) return pni_throw(env, "java.io.IOException");
-    return 0;
+    try {
+        if (idleUs < 0) {
+            fail("setService: negative idle time %d", idleUs);
+            return pni_throw(env, "java.lang.IllegalArgumentException");
+        }
+        if (vpcsum_ctx_set_service((vpcsum_ctx_t*)(intptr_t)ctx, (uint32_t)idleUs) != 0) return pni_throw(env, "java.io.IOException");
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_setService")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_close(PNIEnv_vpcsum_void* env, int64_t ctx) {
-    (void)env;
-    vpcsum_ctx_destroy((vpcsum_ctx_t*)(intptr_t)ctx);
-    return 0;
+    try {
+        (void)env;
+        vpcsum_ctx_destroy((vpcsum_ctx_t*)(intptr_t)ctx);
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_close")
 }
 
 }  // extern "C"

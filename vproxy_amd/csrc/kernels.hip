@@ -393,12 +393,16 @@ __device__ __forceinline__ void wave_sync_lds() {
 __device__ __forceinline__ uint32_t hsum(uint32_t acc, uint32_t w) { return __builtin_amdgcn_sad_u16(w, 0u, acc); }
 
 // Fast-class trips of one team over its packet's chunks [0, nch): U loads per lane issued
-// back to back, then consumed (payload fast path, masked tail, header bitmaps).  The stored
-// checksum fields (verify) are not summed here: the owner lane loads them in phase A.
-template <int TEAM, int U, bool NT>
+// back to back, then consumed (payload fast path, masked tail, header bitmaps).  Verify: the
+// stored checksum fields are one halfword each (the fast class has L3 and L4 at even offsets),
+// held by one lane of the team in its first trip; that lane writes it to the slot's q3.w (st_slot:
+// L4 field, IP field), instead of every lane summing the fields through all trips for a team
+// reduction (two accumulators live across the trip loop: with them the verify build held 95
+// VGPRs, 5 waves per SIMD).
+template <int TEAM, int U, bool VERIFY, bool NT>
 __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, uint32_t boff, int nch, int klo,
                                            uint32_t kfast, int l4hi, const uint4 bm, int tl, uint32_t& acc_l4,
-                                           uint32_t& acc_ip) {
+                                           uint32_t& acc_ip, uint16_t* st_slot) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     for (int rr = 0; rr * TEAM < nch; rr += U) {
         v4u v[U];
@@ -427,6 +431,16 @@ __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, ui
                     acc_ip = hsum(acc_ip, w[j] & hmask((bm.x >> hb) & 3));
                     acc_l4 = hsum(acc_l4, w[j] & hmask((bm.y >> hb) & 3));
                 }
+                if (VERIFY) {
+                    uint32_t sz = 0, sw = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        sz += w[j] & hmask((bm.z >> (hb0 + 2 * j)) & 3);
+                        sw += w[j] & hmask((bm.w >> (hb0 + 2 * j)) & 3);
+                    }
+                    if ((bm.z >> hb0) & 0xffu) st_slot[1] = (uint16_t)fold32(sz);
+                    if ((bm.w >> hb0) & 0xffu) st_slot[0] = (uint16_t)fold32(sw);
+                }
             }
             asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
         }
@@ -452,7 +466,7 @@ __device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uin
     uint32_t h_l4 = 0, h_ip = 0;   // fast class: halfword sums
     if (a.y >> 31) {
         const uint4 bm = sl[1];
-        fast_trips<TEAM, U, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip);
+        fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip, (uint16_t*)&sl[3].w);
     } else if (nch > 0) {
         const uint4 q2 = sl[2], q3 = sl[3];
         PktPlan pl;
@@ -483,9 +497,11 @@ __device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uin
     const uint32_t s_l4 = fold32(team_sum<TEAM>(fold64(acc_l4 + h_l4)));
     const uint32_t s_ip = fold32(team_sum<TEAM>(fold64(acc_ip + h_ip)));
     const uint32_t s_ps = fold32(team_sum<TEAM>(fold64(acc_ps)));
-    uint32_t s_st = 0;
-    if (VERIFY) s_st = fold32(team_sum<TEAM>(fold32(st_l4))) | (fold32(team_sum<TEAM>(fold32(st_ip))) << 16);
-    if (act && tl == 0) sl[0] = make_uint4(s_l4, s_ip, s_ps, s_st);
+    if (VERIFY && !(a.y >> 31) && nch > 0) {   // the slow class's stored fields: team sums, to q3.w too
+        const uint32_t s_st = fold32(team_sum<TEAM>(fold32(st_l4))) | (fold32(team_sum<TEAM>(fold32(st_ip))) << 16);
+        if (act && tl == 0) sl[3].w = s_st;
+    }
+    if (act && tl == 0) sl[0] = make_uint4(s_l4, s_ip, s_ps, 0u);
 }
 
 // Phase B of K2 for one tier: slots [s_begin, s_end) streamed by teams of TEAM lanes, 64/TEAM
@@ -739,8 +755,6 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         int fld = -1;
         int key = 0;
         int n_small = 0, n_cls = 0;   // n_cls: distinct cost classes in the large tier
-        bool fastc = false;           // fast class (header bitmaps; L3 and L4 at even offsets)
-        uint32_t ld_sip = 0, ld_sl4 = 0;   // verify, fast class: the stored fields, loaded in phase A
         bool fastu = false;           // window unit (SF): sums in fsums, no slots
         uint4 fsums = make_uint4(0, 0, 0, 0);
         // Window units (SF): the 64 packets of the unit have one shape (descriptor fields, flags
@@ -802,7 +816,9 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                         for (int u = 0; u < 4; ++u) {
                             const uint32_t f = 64u * u + ln;
                             const uint32_t pk = (f * mul) >> 16;
-                            const uint32_t src = (uint32_t)__shfl((int)boff, (int)(pk & 63u), 64);
+                            // lane (pk & 63)'s boff: one ds_bpermute (no lane-base arithmetic, which
+                            // __shfl adds and the compiler hoists out of the unit loop)
+                            const uint32_t src = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((pk & 63u) << 2), (int)boff);
                             c[u] = __builtin_amdgcn_raw_buffer_load_b128(
                                 rsrc, u < nchw ? src + ((f - pk * (uint32_t)nchw) << 4) : kOutOfRange, 0, NT ? 2 : 0);
                         }
@@ -924,19 +940,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                     if (proto != 1) B_l4 |= (ver == 4) ? hw_range(r0h + 6, r0h + 10) : hw_range(r0h + 4, r0h + 20);
                 }
             }
-            fastc = hbm && klo <= 4;
-            if (VERIFY) {
-                // The stored IP / L4 checksum fields of a fast-class packet (both at even
-                // addresses): two 2-B loads issued now and consumed in phase C, so their latency
-                // hides under phase B.  The teams then stream the packet without summing the fields
-                // through every trip and reducing them (two accumulators and two bitmaps live
-                // across the trip loop: the verify build held 95 VGPRs for it, 80 now).  The
-                // load's line is the one the packet's first chunk comes from (same policy: one
-                // fetch).  The slow class keeps its team sums of the fields.
-                const bool pre = !bad && fastc;
-                ld_sip = __builtin_amdgcn_raw_buffer_load_b16(rsrc, pre && do_ip ? (uint32_t)off + 10u : kOutOfRange, 0, NT ? 2 : 0);
-                ld_sl4 = __builtin_amdgcn_raw_buffer_load_b16(rsrc, pre && do_l4 ? (uint32_t)off + (uint32_t)(l4o + fld) : kOutOfRange, 0, NT ? 2 : 0);
-            }
+            const bool fastc = hbm && klo <= 4;
             // cost class: bad first (key 0), then the small tier (one trip of TS x US chunks),
             // then trips of the large tier's team loop, the slow class last
             if (!bad) {
@@ -989,10 +993,10 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                             }
                         }
                         if (VERIFY) {
-                            const uint32_t s_ip = fastc ? bswap16(ld_sip) : orient(sums.w >> 16, r0);
+                            const uint32_t s_ip = orient(sums.w >> 16, r0);
                             if (do_ip && s_ip == ipc) st |= VPCSUM_S_IP_OK;
                             if (do_l4) {
-                                const uint32_t stored = fastc ? bswap16(ld_sl4) : orient(sums.w & 0xffff, r0 + l4o + fld);
+                                const uint32_t stored = orient(sums.w & 0xffff, r0 + l4o + fld);
                                 if (stored == l4c) st |= VPCSUM_S_L4_OK;
                                 if (!psonly && proto == 17 && stored == 0) st |= VPCSUM_S_UDP_NOCSUM;
                             }
@@ -1037,6 +1041,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         // after the stores would stall the wave until they complete, once per unit.
         asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
         sums = s_slot[wid][key][0];
+        if (VERIFY) sums.w = s_slot[wid][key][3].w;   // stored fields {l4, ip << 16}
         }
         if (!fastu) finish(sums);
         wave_sync_lds();   // slots are rewritten by the next super-iteration

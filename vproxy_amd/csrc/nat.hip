@@ -670,8 +670,11 @@ static uint32_t nat_grid(uint32_t n, int wl2, uint32_t wgs_per_cu) {
 }
 
 // Internal tuning bits of nat_mode (not part of the stable ABI): bit 8 byte-access kernel; bits
-// 12..14 log2(packets per lane) + 1 of the wide kernel; bits 16..17 window chunks (1: 6, 2: 4);
-// bits 18..22 workgroups per CU (0: 24); bit 23 the lane layout (k_natw) instead of quads (k_natq).
+// 12..14 log2(packets per lane) + 1 of the wide kernel (k_natw takes 1, 2 or 4 packets per lane;
+// k_natq only 1 or 2, so a request for 4 runs k_natq at 2); bits 16..17 window chunks (1: 6,
+// 2: 4); bits 18..22 workgroups per CU (0: 24); bit 23 the lane layout (k_natw) instead of quads
+// (k_natq); bits 24..25 k_natq's forced occupancy (1: 6, 2: 8 waves per SIMD -- tuning shapes that
+// may spill to scratch, tests/test_kernel_resources.py exempts them; 0 and 3: the default).
 static int nat_chunks_sel(uint32_t nat_mode, int fmt) {
     const uint32_t c = (nat_mode >> 16) & 3u;
     if (c == 1) return 6;

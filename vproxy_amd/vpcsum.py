@@ -22,6 +22,7 @@ S_TTL_EXPIRED = 0x20
 MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
 NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL, NAT_SET_TTL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 NAT_RFC1624, NAT_STRICT_JAVA = 0x00, 0x01
+ABI_VERSION = 2   # include/vpcsum.h VPCSUM_ABI_VERSION: the library this binding was written against
 SYNTH_C1, SYNTH_C2, SYNTH_C3, SYNTH_C4, SYNTH_FUZZ, SYNTH_C5 = 1, 2, 3, 4, 5, 6
 
 DESC_DTYPE = np.dtype([("l3_off", "<u8"), ("l3_len", "<u2"), ("l4_off", "<u2"), ("l3_ver", "u1"),
@@ -141,7 +142,7 @@ def lib():
             except OSError as e:
                 raise VpcsumUnavailable(f"cannot load {LIB}: {e}") from e
             _declare(L)
-            if L.vpcsum_abi_version() != 1:
+            if L.vpcsum_abi_version() != ABI_VERSION:
                 raise VpcsumUnavailable("ABI version mismatch")
             _lib = L
         return _lib
