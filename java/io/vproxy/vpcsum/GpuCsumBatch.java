@@ -33,6 +33,15 @@ import java.lang.foreign.ValueLayout;
  *
  * One instance per event loop: like everything on the vswitch data path it is single-threaded
  * (Switch.java:170-199).  Not compiled in this repository (no JDK in the build image).
+ *
+ * The status segment that {@link #nat}, {@link #verify} and {@link #verifyFrames} return is this
+ * instance's own buffer: it is valid until the next call on this instance (the next flush, NAT or
+ * verify overwrites it).  Copy what must outlive that, or pass your own segment to the overloads
+ * that take one.
+ *
+ * {@link #stats} counts where every deferred frame went (GPU, small-flush hand-back, rejected
+ * descriptor hand-back), next to IfaceStatistics: with INTEGRATION.md §3's diff the interface keeps
+ * counting csum_skip for every frame whose sums Java left to someone else, the GPU included.
  */
 public final class GpuCsumBatch implements AutoCloseable {
     private static final int DESC = 16;
@@ -57,6 +66,28 @@ public final class GpuCsumBatch implements AutoCloseable {
     private final int[] frameNativeFlags;
     private int nFrames = 0;
 
+    /** Where the deferred frames went (cumulative).  Invariant after a flush:
+     * deferred == gpuHandled + smallFlushHandedBack + badDescHandedBack. */
+    public static final class Stats {
+        public long deferred;              // frames taken over by defer / deferFrame
+        public long gpuHandled;            // frames the GPU wrote
+        public long smallFlushHandedBack;  // frames of flushes below SMALL_FLUSH, back to vpxdp
+        public long badDescHandedBack;     // frames the kernel refused (S_BAD_DESC), back to vpxdp
+        public long gpuFlushes;            // flushes that went to the GPU
+
+        @Override
+        public String toString() {
+            return "csum_deferred=" + deferred + " csum_gpu=" + gpuHandled + " csum_small_flush=" + smallFlushHandedBack
+                   + " csum_bad_desc=" + badDescHandedBack + " csum_gpu_flushes=" + gpuFlushes;
+        }
+    }
+
+    private final Stats stats = new Stats();
+
+    public Stats stats() {
+        return stats;
+    }
+
     /** Flushes of fewer frames go back to the native VP_CSUM_* path (the GPU breaks even at about
      * 5 frames per flush with the service grid, DESIGN.md §8). */
     public static final int SMALL_FLUSH = 5;
@@ -65,9 +96,14 @@ public final class GpuCsumBatch implements AutoCloseable {
         this.umem = umem;
         this.umemLen = umem.byteSize();
         this.capacity = capacity;
+        if (VPCsum.get().abiVersion() != VPCsum.ABI_VERSION) {
+            throw new IOException("libvpcsum ABI " + VPCsum.get().abiVersion() + ", binding expects " + VPCsum.ABI_VERSION);
+        }
         this.ctx = VPCsum.get().create(env, device, umemLen, capacity);
         VPCsum.get().registerArena(env, ctx, umem, umemLen);
-        // completeTx flushes are small: keep a resident GPU grid polling for them (20 ms idle)
+        // completeTx flushes are small: keep a resident GPU grid polling for them (20 ms idle).
+        // Until it leaves, that grid is device work: a hipDeviceSynchronize or hipFree by another
+        // user of this GPU in this process waits up to 20 ms for it (INTEGRATION.md §7)
         VPCsum.get().setService(env, ctx, 20_000);
         this.desc = arena.allocate((long) DESC * capacity, 16);
         this.out = arena.allocate(4L * capacity, 16);
@@ -110,6 +146,7 @@ public final class GpuCsumBatch implements AutoCloseable {
         frameChunks[nFrames] = chunk;
         frameNativeFlags[nFrames] = nativeFlags;
         ++nFrames;
+        ++stats.deferred;
         return keep;
     }
 
@@ -183,6 +220,7 @@ public final class GpuCsumBatch implements AutoCloseable {
         chunks[n] = chunk;
         nativeFlagsOf[n] = nativeFlags;
         ++n;
+        ++stats.deferred;
         return keep;
     }
 
@@ -207,6 +245,7 @@ public final class GpuCsumBatch implements AutoCloseable {
                 frameChunks[i].setCsumFlags(frameNativeFlags[i]);
                 frameChunks[i] = null;
             }
+            stats.smallFlushHandedBack += nFrames;
             nFrames = 0;
             return 0;
         }
@@ -219,6 +258,9 @@ public final class GpuCsumBatch implements AutoCloseable {
             }
             frameChunks[i] = null;
         }
+        stats.gpuHandled += done;
+        stats.badDescHandedBack += nFrames - done;
+        ++stats.gpuFlushes;
         nFrames = 0;
         return done;
     }
@@ -233,6 +275,7 @@ public final class GpuCsumBatch implements AutoCloseable {
                 chunks[i].setCsumFlags(nativeFlagsOf[i]);
                 chunks[i] = null;
             }
+            stats.smallFlushHandedBack += n;
             n = 0;
             return 0;
         }
@@ -245,6 +288,9 @@ public final class GpuCsumBatch implements AutoCloseable {
             }
             chunks[i] = null;
         }
+        stats.gpuHandled += done;
+        stats.badDescHandedBack += n - done;
+        ++stats.gpuFlushes;
         n = 0;
         return done;
     }
@@ -253,36 +299,56 @@ public final class GpuCsumBatch implements AutoCloseable {
      * SwitchUtils.applyNat for a batch of frames in the umem (SwitchUtils.java:522-542): each
      * 48-byte entry of {@code rw} (addresses, ports, TTL / hop limit; VPCsum.NAT_*) rewrites the
      * packet of the matching descriptor of {@code natDesc} in place, checksums updated as the
-     * setters + getRawPacket(0) would leave them.  Returns one status byte per packet.
+     * setters + getRawPacket(0) would leave them.  Returns one status byte per packet in this
+     * instance's status segment, valid until the next call on this instance (see the class note).
      */
     public MemorySegment nat(MemorySegment natDesc, MemorySegment rw, int count, boolean strictJava) throws IOException {
-        long t = VPCsum.get().natSubmit(env, ctx, umem, umemLen, natDesc, rw, count, status,
+        return nat(natDesc, rw, count, strictJava, status);
+    }
+
+    /** {@link #nat} with the status bytes written to the caller's {@code statusOut} (count bytes). */
+    public MemorySegment nat(MemorySegment natDesc, MemorySegment rw, int count, boolean strictJava,
+                             MemorySegment statusOut) throws IOException {
+        long t = VPCsum.get().natSubmit(env, ctx, umem, umemLen, natDesc, rw, count, statusOut,
             strictJava ? VPCsum.NAT_STRICT_JAVA : VPCsum.NAT_RFC1624);
         VPCsum.get().waitFor(env, ctx, t);
-        return status;
+        return statusOut;
     }
 
     /**
      * Ingress verify of {@code count} frames already described in {@code desc} (e.g. built by the
      * GPU parser, vpcsum_parse_ether_async): fills {@code status} (S_IP_OK / S_L4_OK /
-     * S_UDP_NOCSUM per frame) without touching the frames.
+     * S_UDP_NOCSUM per frame) without touching the frames.  The returned segment is this
+     * instance's, valid until the next call on it (see the class note).
      */
     public MemorySegment verify(MemorySegment frameDesc, int count) throws IOException {
-        long t = VPCsum.get().submit(env, ctx, umem, umemLen, frameDesc, count, out, status, VPCsum.MODE_VERIFY);
+        return verify(frameDesc, count, status);
+    }
+
+    /** {@link #verify} with the status bytes written to the caller's {@code statusOut} (count bytes). */
+    public MemorySegment verify(MemorySegment frameDesc, int count, MemorySegment statusOut) throws IOException {
+        long t = VPCsum.get().submit(env, ctx, umem, umemLen, frameDesc, count, out, statusOut, VPCsum.MODE_VERIFY);
         VPCsum.get().waitFor(env, ctx, t);
-        return status;
+        return statusOut;
     }
 
     /**
      * Ingress verify straight from the RX ring (XDPIface.readable, XDPIface.java:281-314): the
      * {@code count} received frames at umem offsets {@code frameOff} (u64 each) with lengths
      * {@code frameLen} (u32 each) are parsed and verified on the GPU in one submission, without
-     * building descriptors in Java.  Returns one status byte per frame.
+     * building descriptors in Java.  Returns one status byte per frame, in this instance's
+     * segment, valid until the next call on it (see the class note).
      */
     public MemorySegment verifyFrames(MemorySegment frameOff, MemorySegment frameLen, int count) throws IOException {
-        long t = VPCsum.get().verifyFrames(env, ctx, umem, umemLen, frameOff, frameLen, count, out, status);
+        return verifyFrames(frameOff, frameLen, count, status);
+    }
+
+    /** {@link #verifyFrames} with the status bytes written to the caller's {@code statusOut}. */
+    public MemorySegment verifyFrames(MemorySegment frameOff, MemorySegment frameLen, int count,
+                                      MemorySegment statusOut) throws IOException {
+        long t = VPCsum.get().verifyFrames(env, ctx, umem, umemLen, frameOff, frameLen, count, out, statusOut);
         VPCsum.get().waitFor(env, ctx, t);
-        return status;
+        return statusOut;
     }
 
     /**

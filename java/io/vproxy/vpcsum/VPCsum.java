@@ -4,7 +4,11 @@ import io.vproxy.pni.PNIEnv;
 import io.vproxy.pni.PNILinkOptions;
 import io.vproxy.pni.PanamaUtils;
 
+import java.lang.foreign.FunctionDescriptor;
+import java.lang.foreign.Linker;
 import java.lang.foreign.MemorySegment;
+import java.lang.foreign.SymbolLookup;
+import java.lang.foreign.ValueLayout;
 import java.lang.invoke.MethodHandle;
 
 /**
@@ -33,6 +37,22 @@ public class VPCsum {
 
     public static VPCsum get() {
         return INSTANCE;
+    }
+
+    /** include/vpcsum.h VPCSUM_ABI_VERSION this binding was written against (2: NAT_DEC_TTL refuses
+     * TTL <= 1 with S_TTL_EXPIRED).  {@link #abiVersion} reports the loaded library's. */
+    public static final int ABI_VERSION = 2;
+
+    private static final MethodHandle abiVersionMH = Linker.nativeLinker().downcallHandle(
+        SymbolLookup.loaderLookup().find("vpcsum_abi_version").orElseThrow(), FunctionDescriptor.of(ValueLayout.JAVA_INT));
+
+    /** vpcsum_abi_version() of the loaded library (a plain C function, no PNIEnv). */
+    public int abiVersion() {
+        try {
+            return (int) abiVersionMH.invokeExact();
+        } catch (Throwable THROWABLE) {
+            throw new IllegalStateException("vpcsum_abi_version", THROWABLE);
+        }
     }
 
     // descriptor flags (include/vpcsum.h)

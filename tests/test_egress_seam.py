@@ -106,6 +106,11 @@ def test_egress_rejected_descriptor_is_handed_back(V, orc):
         batch.defer_frame(oo, fl)
     assert batch.complete_tx() == 39
     assert batch.stats["rejected"] == 1
+    # GpuCsumBatch.stats(): every deferred frame is accounted for, and the interface's csum_skip
+    #  counts all 40, the GPU's and the handed-back one alike
+    st = batch.stats
+    assert (st["tx_csum_skip"], st["deferred"], st["gpu_handled"], st["bad_desc_handed_back"],
+            st["small_flush_handed_back"]) == (40, 40, 39, 1, 0)
     assert len(batch.handed_back) == 1 and int(batch.handed_back[0][0]["l3_off"]) == o + hl
     assert np.array_equal(arena[o:o + 128], before7)
     assert np.array_equal(arena, want)
@@ -190,3 +195,50 @@ def test_egress_descriptor_random_frames():
         got = (int(d["l3_off"]), int(d["l3_len"]), int(d["l4_off"]), int(d["l3_ver"]), int(d["l4_proto"]), int(d["flags"]))
         assert got == want, (i, got, want)
     assert n_ok > 1500
+
+
+@pytest.mark.gpu
+def test_egress_counters_small_flush_and_frames(V, orc):
+    """The counters of both egress mirrors (GpuCsumBatch.stats in Java): a flush below the small-
+    flush threshold hands its frames back and counts them as such; the raw-frame batch counts GPU
+    frames and refusals; frames without dirty sums are not counted as skipped."""
+    from vproxy_amd import vswitch as S
+    fs, arena, offs, flags = _batch()
+    b = S.EgressBatch(arena.copy(), capacity=16, small_flush=5)
+    for o, fl in zip(offs[:3], flags[:3]):
+        assert b.defer_frame(o, fl)
+    assert not b.defer_frame(offs[3], 0)          # nothing dirty: the chunk keeps flags 0
+    assert b.complete_tx() == 0
+    st = b.stats
+    assert (st["tx_pkts"], st["tx_csum_skip"], st["deferred"], st["gpu_handled"], st["small_flush_handed_back"],
+            st["flushes"]) == (4, 3, 3, 0, 3, 0)
+    b.close()
+    a2 = arena.copy()
+    fb = S.FrameEgressBatch(a2, capacity=64)
+    for f, o, fl in zip(fs[:20], offs[:20], flags[:20]):
+        assert fb.defer(o, len(f["frame"]), fl)
+    fb.defer(offs[20], 10, flags[20])             # 10 B: no IP header, the GPU refuses it
+    assert fb.complete_tx() == 20
+    assert (fb.stats["tx_csum_skip"], fb.stats["deferred"], fb.stats["gpu_handled"],
+            fb.stats["bad_desc_handed_back"], fb.stats["flushes"]) == (21, 21, 20, 1, 1)
+    fb.close()
+
+
+def test_egress_descriptor_short_frames_and_ext_chains():
+    """egress_descriptor never reads past the bytes it is given (a frame within 64 B of the arena
+    end), and an IPv6 chain of two extension headers yields the second header as l4_proto (refused
+    by the kernel, so handed back), as the GPU parser refuses such a frame."""
+    from vproxy_amd import vswitch as S
+    assert S.egress_descriptor(np.zeros(10, np.uint8), 0, 3) is None
+    v4 = np.zeros(30, np.uint8)
+    v4[12:14] = [0x08, 0x00]
+    assert S.egress_descriptor(v4, 0, 3) is None            # 16 B of a 20-B IPv4 header
+    v6 = np.zeros(64, np.uint8)
+    v6[12:14] = [0x86, 0xdd]
+    v6[14] = 0x60
+    v6[14 + 4:14 + 6] = [0, 24]
+    v6[14 + 6] = 0                                        # hop-by-hop ...
+    v6[14 + 40] = 60                                      # ... then destination options
+    d = S.egress_descriptor(v6, 0, 2)
+    assert int(d["l4_proto"]) == 60 and int(d["l4_off"]) == 48
+    assert S.egress_descriptor(v6[:54], 0, 2) is None      # the extension header cut off

@@ -1407,7 +1407,70 @@ def test_group_register_unregister_cycle(V, orc):
         g.unregister(arena)
     out, _ = g.run(arena, desc)
     assert np.array_equal(out, want)
+    # a zero-copy batch still in flight on the arena: unregister finishes it on every context first
+    # (phase 1), then drops the mappings and unpins (phase 2); the results are whole
+    g.register(arena)
+    out = np.zeros(len(desc), np.uint32)
+    t = g.submit(arena, desc, out, None, O.MODE_COMPUTE)
+    g.unregister(arena)
+    g.wait(t)
+    assert np.array_equal(out, want)
+    g.register(arena)   # and it registers again
+    g.unregister(arena)
     g.close()
+
+
+def test_default_group_threads_race_shutdown(V, orc):
+    """vpcsum_batch_submit / vpcsum_batch_wait from several threads while another thread shuts the
+    process-wide group down and re-initialises it: every call either completes with the oracle's
+    results or fails with "vpcsum_init first" -- never a use-after-free (the group is held
+    under a shared lock for each call, shutdown takes it exclusively)."""
+    import ctypes
+    import threading
+    import torch
+    L = V.lib()
+    mask = 1
+    arena, d = orc.synth(512, 2048, 14, O.SYNTH_C3, O.SEED, 2024)
+    want, _ = orc.process(arena, d)
+    errors, done = [], [0]
+    stop = threading.Event()
+
+    def worker():
+        out = np.zeros(len(d), np.uint32)
+        h = ctypes.c_uint64()
+        while not stop.is_set():
+            out[:] = 0
+            if L.vpcsum_batch_submit(arena.ctypes.data, arena.nbytes, d.ctypes.data, len(d), out.ctypes.data, None,
+                                     0, ctypes.byref(h)) != 0:
+                msg = L.vpcsum_last_error().decode()
+                if "vpcsum_init first" not in msg:
+                    errors.append(msg)
+                continue
+            if L.vpcsum_batch_wait(h.value) != 0:
+                msg = L.vpcsum_last_error().decode()
+                if "vpcsum_init first" not in msg:
+                    errors.append(msg)
+                continue
+            if not np.array_equal(out, want):
+                errors.append("wrong results")
+            done[0] += 1
+
+    assert L.vpcsum_init(mask, arena.nbytes, len(d)) == 0
+    ts = [threading.Thread(target=worker) for _ in range(4)]
+    for t in ts:
+        t.start()
+    try:
+        for _ in range(20):
+            assert L.vpcsum_shutdown() == 0
+            assert L.vpcsum_init(mask, arena.nbytes, len(d)) == 0
+    finally:
+        stop.set()
+        for t in ts:
+            t.join(60)
+        L.vpcsum_shutdown()
+    torch.cuda.synchronize()
+    assert not errors, errors[:5]
+    assert done[0] > 0
 
 
 def test_full_size_c5_properties(V, orc):

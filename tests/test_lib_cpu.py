@@ -119,3 +119,30 @@ def test_allocation_failure_returns_error(libpath, tmp_path):
                            "-lvpcsum", "-Wl,-rpath," + os.path.dirname(libpath), "-o", str(exe)])
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "out of host memory" in r.stdout, (r.returncode, r.stdout, r.stderr)
+
+
+def test_default_group_calls_race_shutdown_without_gpu(libpath):
+    """The process-wide group's entry points from several threads racing vpcsum_shutdown (no GPU
+    here, so every call is refused): no crash, every refusal says "vpcsum_init first"."""
+    import threading
+    L = ctypes.CDLL(libpath)
+    L.vpcsum_last_error.restype = ctypes.c_char_p
+    bad = []
+
+    def worker():
+        h = ctypes.c_uint64()
+        for _ in range(2000):
+            if L.vpcsum_batch_submit(None, ctypes.c_uint64(0), None, ctypes.c_uint32(0), None, None,
+                                     ctypes.c_uint32(0), ctypes.byref(h)) == 0 or \
+                    b"vpcsum_init first" not in L.vpcsum_last_error():
+                bad.append(1)
+            L.vpcsum_batch_wait(ctypes.c_uint64(1))
+
+    ts = [threading.Thread(target=worker) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for _ in range(2000):
+        assert L.vpcsum_shutdown() == 0
+    for t in ts:
+        t.join()
+    assert not bad

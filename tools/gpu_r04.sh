@@ -70,6 +70,13 @@ if has rank8; then   # 8 ranks on one card: the strong shards per rank, a functi
   step bench_c4s_8rank 600 python bench.py --workload c4 --strong --gpus 8 --steps 50 --warmup 5 --share-gpu --ramp-ms 300
   step bench_c5_8rank 600 python bench.py --workload c5 --gpus 8 --steps 20 --warmup 3 --share-gpu --ramp-ms 300
 fi
+if has pmcmode; then   # compute vs verify counters of the default kernel (PMC_CFGS, default c1)
+  M="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES SQ_WAIT_INST_ANY SQ_WAVE_CYCLES|FETCH_SIZE|WRITE_SIZE|SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_WR SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+  for w in ${PMC_CFGS:-c1}; do for m in 0 1; do
+    IFS='|' read -ra PS <<< "$M"; i=0
+    for c in "${PS[@]}"; do i=$((i+1)); step pmcm_${w}_m${m}_p$i 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmcm_${w}_m$m -o p$i -- python3 tools/prof_one.py --workload $w --mode $m; done
+  done; done
+fi
 if has ab; then   # this tree's library against vproxy_amd/libvpcsum_ab.so, uncached batches, compute + verify
   step ab 1100 bash tools/ab_libs_cold.sh ${TAG}_ab "${AB_WS:-c1 c3 c2}" ${AB_ROUNDS:-2} "${AB_MODES:-0 1}"
 fi

@@ -8,6 +8,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c2")
 ap.add_argument("--variants", default="0")
 ap.add_argument("--bpc", type=int, default=0)
+ap.add_argument("--mode", type=int, default=0, help="checksum mode: 0 compute (out only), 1 verify (out + status)")
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--nat", type=int, default=-1, help="nat_mode: profile vpcsum_nat4_async on C5 instead")
 ap.add_argument("--nat-mask", type=int, default=0x0F, help="rewrite mask of every entry (0: read-only pass)")
@@ -39,8 +40,9 @@ arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
 d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
 V.synth(arena, n, stride, 0, sid, 0x20241020, 0, d)
 out = torch.zeros(n, dtype=torch.int32, device="cuda")
+st = torch.zeros(n, dtype=torch.uint8, device="cuda") if a.mode == 1 else None
 for v in map(int, a.variants.split(",")):
     for _ in range(a.iters):
-        V.compute(arena, d, n, out, None, 0, v, blocks_per_cu=a.bpc)
+        V.compute(arena, d, n, out, st, a.mode, v, blocks_per_cu=a.bpc)
 torch.cuda.synchronize()
 print("done")

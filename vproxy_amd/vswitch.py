@@ -63,23 +63,39 @@ def egress_descriptor(frame, frame_off: int, flags: int):
       8 + hdrExtLen per extension header, which from() fills whenever the next header is one,
       :33-35), l4_proto = getProtocol() (the last header's next header, :363-367).
 
-    `frame` holds the frame's bytes from its first byte: the header fields the Java object
-    exposes are read from it (no checksum is computed here).  Returns a DESC_DTYPE record, or None
-    for a frame that is not IP."""
+    An IPv6 chain of two or more extension headers never reaches the seam in vproxy (Ipv6Packet.from
+    loops on it), and the GPU parser refuses it: here the descriptor names the second
+    extension header as l4_proto, which the kernel refuses with F_L4 (S_BAD_DESC), so such a frame is
+    handed back to the native path.
+
+    `frame` holds the frame's bytes from its first byte (at least its headers: a frame near the end
+    of the arena may be shorter than 64 B): the header fields the Java object exposes are read from
+    it (no checksum is computed here).  Returns a DESC_DTYPE record, or None for a frame that is not
+    IP or too short to hold its IP header."""
     b = frame
+    if len(b) < 14:
+        return None
     typ, hl = _u16(b, 12), 14
     if typ == ETHER_TYPE_8021Q:
+        if len(b) < 18:
+            return None
         typ, hl = _u16(b, 16), 18
     d = np.zeros(1, V.DESC_DTYPE)[0]
     d["l3_off"] = frame_off + hl
     d["flags"] = flags
     if typ == ETHER_TYPE_IPv4:
+        if len(b) < hl + 20:
+            return None
         d["l3_len"] = _u16(b, hl + 2)
         d["l4_off"] = (int(b[hl]) & 0x0F) * 4
         d["l3_ver"], d["l4_proto"] = 4, int(b[hl + 9])
     elif typ == ETHER_TYPE_IPv6:
+        if len(b) < hl + 40:
+            return None
         nh, off = int(b[hl + 6]), 40
         if nh in IPV6_EXT_HEADERS:   # one extension header (a chain makes Java's parser loop)
+            if len(b) < hl + 42:
+                return None
             nh, off = int(b[hl + 40]), 40 + 8 + int(b[hl + 41])
         d["l3_len"] = 40 + _u16(b, hl + 4)
         d["l4_off"] = off
@@ -116,32 +132,45 @@ class EgressBatch:
         self.out = np.zeros(capacity, np.uint32)
         self.status = np.zeros(capacity, np.uint8)
         self.n = 0
-        self.stats = {"tx_pkts": 0, "tx_csum_gpu": 0, "flushes": 0}
+        # GpuCsumBatch.stats(): tx_csum_skip is what IfaceStatistics.txCsumSkip counts with
+        # INTEGRATION.md §3's diff (every frame whose sums Java left to someone else: the GPU or the
+        # native path, XDPIface.java:117-120, 161-164); the rest say who took them.  Invariant:
+        # deferred == gpu_handled + small_flush_handed_back + bad_desc_handed_back + pending.
+        self.stats = {"tx_pkts": 0, "tx_csum_skip": 0, "deferred": 0, "gpu_handled": 0, "tx_csum_gpu": 0,
+                      "small_flush_handed_back": 0, "bad_desc_handed_back": 0, "handed_back": 0, "rejected": 0,
+                      "flushes": 0}
+
+    def _take(self, flags: int) -> bool:
+        self.stats["tx_pkts"] += 1
+        if flags == 0:
+            return False
+        self.stats["tx_csum_skip"] += 1
+        return True
 
     def defer(self, l3_off: int, l3_len: int, l4_off: int, ver: int, proto: int, flags: int) -> bool:
         """Record a frame whose sums are dirty.  Returns False (nothing to do) when flags == 0."""
-        self.stats["tx_pkts"] += 1
-        if flags == 0:
+        if not self._take(flags):
             return False
         if self.n == self.capacity:
             self.complete_tx()
         self.desc[self.n] = (l3_off, l3_len, l4_off, ver, proto, flags, 0)
         self.n += 1
+        self.stats["deferred"] += 1
         return True
 
     def defer_frame(self, frame_off: int, flags: int) -> bool:
         """GpuCsumBatch.defer for a frame at `frame_off` of the arena: the descriptor comes from
         the IP header fields (:func:`egress_descriptor`), never from the buffer length."""
-        self.stats["tx_pkts"] += 1
-        if flags == 0:
+        if not self._take(flags):
             return False
         d = egress_descriptor(self.arena[frame_off:frame_off + 64], frame_off, flags)
-        if d is None:
+        if d is None:   # not IP: the chunk keeps its native flags
             return False
         if self.n == self.capacity:
             self.complete_tx()
         self.desc[self.n] = d
         self.n += 1
+        self.stats["deferred"] += 1
         return True
 
     def complete_tx(self) -> int:
@@ -154,7 +183,8 @@ class EgressBatch:
         n = self.n
         if n < self.small_flush:
             self.handed_back.append(self.desc[:n].copy())
-            self.stats["handed_back"] = self.stats.get("handed_back", 0) + n
+            self.stats["handed_back"] += n
+            self.stats["small_flush_handed_back"] += n
             self.n = 0
             return 0
         t = self.ctx.submit(self.arena, self.desc[:n], self.out[:n], self.status[:n], V.MODE_WRITE)
@@ -163,9 +193,11 @@ class EgressBatch:
         nbad = int(np.count_nonzero(bad))
         if nbad:
             self.handed_back.append(self.desc[:n][bad].copy())
-            self.stats["handed_back"] = self.stats.get("handed_back", 0) + nbad
-            self.stats["rejected"] = self.stats.get("rejected", 0) + nbad
+            self.stats["handed_back"] += nbad
+            self.stats["rejected"] += nbad
+            self.stats["bad_desc_handed_back"] += nbad
         self.stats["tx_csum_gpu"] += n - nbad
+        self.stats["gpu_handled"] += n - nbad
         self.stats["flushes"] += 1
         self.n = 0
         return n - nbad
@@ -192,14 +224,17 @@ class FrameEgressBatch:
         self.flags = np.zeros(capacity, np.uint8)
         self.n = 0
         self.handed_back: list[tuple[int, int, int]] = []
+        self.stats = {"tx_csum_skip": 0, "deferred": 0, "gpu_handled": 0, "bad_desc_handed_back": 0, "flushes": 0}
 
     def defer(self, frame_off: int, frame_len: int, flags: int) -> bool:
         if flags == 0:
             return False
+        self.stats["tx_csum_skip"] += 1
         if self.n == self.capacity:
             self.complete_tx()
         self.off[self.n], self.len[self.n], self.flags[self.n] = frame_off, frame_len, flags
         self.n += 1
+        self.stats["deferred"] += 1
         return True
 
     def complete_tx(self) -> int:
@@ -209,6 +244,9 @@ class FrameEgressBatch:
         _, st = self.ctx.egress_frames(self.arena, self.off[:n], self.len[:n], self.flags[:n])
         bad = np.nonzero(st & V.S_BAD_DESC)[0]
         self.handed_back += [(int(self.off[i]), int(self.len[i]), int(self.flags[i])) for i in bad]
+        self.stats["gpu_handled"] += n - len(bad)
+        self.stats["bad_desc_handed_back"] += len(bad)
+        self.stats["flushes"] += 1
         self.n = 0
         return n - len(bad)
 
