@@ -285,6 +285,36 @@ def _gpu_nat(V, arena_np, desc, rw, mode):
     return arena.cpu().numpy(), st.cpu().numpy()
 
 
+def _gpu_nat_rec(V, arena_np, desc, rw, mode):
+    import torch
+    arena = dev(arena_np.copy())
+    rec = np.zeros(len(desc), V.NAT4R_DTYPE)
+    rec["desc"], rec["rw"] = desc, rw
+    st = torch.zeros(len(desc), dtype=torch.uint8, device="cuda")
+    V.nat4r(arena, dev(rec.view(np.uint8)), len(desc), st, mode)
+    torch.cuda.synchronize()
+    return arena.cpu().numpy(), st.cpu().numpy()
+
+
+@pytest.mark.parametrize("pad", [0, 2, 14])
+@pytest.mark.parametrize("workload", [O.SYNTH_C3, O.SYNTH_FUZZ, O.SYNTH_C5])
+@pytest.mark.parametrize("packed", [False, True])
+def test_nat_records_against_java(V, orc, pad, workload, packed):
+    """vpcsum_nat4r_async (vpcsum_nat4_rec_t: descriptor + IPv4 entry in one 32-B record) on every
+    kernel shape equals the Java restatement byte for byte (IPv6 refused, TTL-expired refused,
+    UDP stored 0 recomputed); the strict-Java mode is refused for records."""
+    n = 1500 if workload == O.SYNTH_FUZZ else 3000
+    arena, desc, rw = _nat_batch(orc, n, seed=pad + 71, udp_zero=0.1, pad=pad, workload=workload, packed=packed)
+    want = arena.copy()
+    want_st = orc.nat4_java(want, desc, rw)
+    for tune in (0, 0x100, 0x1000, 0x3000, 0x20000, 0x23000, 0x800000, 0x801000, 0x20000 | (3 << 18)):
+        got, st = _gpu_nat_rec(V, arena, desc, rw, V.NAT_RFC1624 | tune)
+        assert np.array_equal(st, want_st), tune
+        assert np.array_equal(got, want), tune
+    with pytest.raises(V.VpcsumError, match="RFC_1624|RFC 1624"):
+        _gpu_nat_rec(V, arena, desc, rw, V.NAT_STRICT_JAVA)
+
+
 def test_nat_rfc1624_bit_exact_on_valid_input(V, orc):
     arena, desc, rw = _nat_batch(orc, 4000, udp_zero=0.1)
     want = arena.copy()

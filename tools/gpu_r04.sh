@@ -77,6 +77,9 @@ if has pmcmode; then   # compute vs verify counters of the default kernel (PMC_C
     for c in "${PS[@]}"; do i=$((i+1)); step pmcm_${w}_m${m}_p$i 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmcm_${w}_m$m -o p$i -- python3 tools/prof_one.py --workload $w --mode $m; done
   done; done
 fi
+if has natrec; then   # two-stream NAT vs 32-B records, and their probes, one process, interleaved
+  step natrec 600 python tools/natsweep.py --rec --rounds 4
+fi
 if has ab; then   # this tree's library against vproxy_amd/libvpcsum_ab.so, uncached batches, compute + verify
   step ab 1100 bash tools/ab_libs_cold.sh ${TAG}_ab "${AB_WS:-c1 c3 c2}" ${AB_ROUNDS:-2} "${AB_MODES:-0 1}"
 fi

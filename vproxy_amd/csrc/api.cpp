@@ -279,6 +279,7 @@ static int nat_async(const char* what, uint8_t* d_arena, uint64_t arena_len, con
     // instead of quads, bits 24..25 the quad kernel's forced occupancy (6 / 8 waves: may spill)
     if (nat_mode & ~(VPCSUM_NAT_STRICT_JAVA | 0x100u | 0x7000u | 0x3ff0000u)) return fail("%s: bad nat_mode 0x%x", what, nat_mode);
     if ((nat_mode & VPCSUM_NAT_STRICT_JAVA) && !d_status) return fail("%s: strict-java mode needs a status buffer", what);
+    if ((nat_mode & VPCSUM_NAT_STRICT_JAVA) && fmt == 2) return fail("%s: records take VPCSUM_NAT_RFC1624 only", what);
     return nat_run(d_arena, arena_len, d_desc, d_rw, fmt, n, d_status, nat_mode, (hipStream_t)stream);
 }
 
@@ -298,6 +299,25 @@ int vpcsum_nat4_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t*
     try {
         return nat_async("vpcsum_nat4_async", d_arena, arena_len, d_desc, d_rw, 0, n, d_status, nat_mode, stream);
     } VPC_CATCH("vpcsum_nat4_async")
+}
+
+int vpcsum_nat4r_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_nat4_rec_t* d_rec, uint32_t n,
+                       uint8_t* d_status, uint32_t nat_mode, void* stream) {
+    try {
+        return nat_async("vpcsum_nat4r_async", d_arena, arena_len, (const vpcsum_desc_t*)d_rec, d_rec, 2, n, d_status,
+                         nat_mode, stream);
+    } VPC_CATCH("vpcsum_nat4r_async")
+}
+
+int vpcsum_nat4r_pattern_probe_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_nat4_rec_t* d_rec,
+                                     uint32_t n, void* stream) {
+    try {
+        if (n == 0) return 0;
+        if (!d_arena || !d_rec) return fail("vpcsum_nat4r_pattern_probe_async: NULL argument");
+        VPC_CHECK(launch_nat_probe(d_arena, arena_len, (const vpcsum_desc_t*)d_rec, d_rec, 2, n, (hipStream_t)stream),
+                  "vpcsum_nat4r_pattern_probe_async launch");
+        return 0;
+    } VPC_CATCH("vpcsum_nat4r_pattern_probe_async")
 }
 
 int vpcsum_nat_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const vpcsum_nat_t* d_rw,

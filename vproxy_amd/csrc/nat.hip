@@ -14,8 +14,9 @@
 // VPCSUM_NAT_STRICT_JAVA rewrites only and hands the dirty flags to the checksum kernel, which
 // recomputes in full: identical to Java for any input.
 //
-// Two rewrite-entry formats: vpcsum_nat4_t (16 B, IPv4 only: BASELINE config C5's 72 B/packet)
-// and vpcsum_nat_t (48 B, IPv4 and IPv6).  One lane per packet for the rewrite; the default wide
+// Three rewrite-entry formats: vpcsum_nat4_t (16 B, IPv4 only: BASELINE config C5's 72 B/packet),
+// vpcsum_nat_t (48 B, IPv4 and IPv6), and vpcsum_nat4_rec_t (FMT 2: the descriptor and the IPv4
+// entry in one 32-B record, so a packet's rewrite comes from one read stream instead of two).  One lane per packet for the rewrite; the default wide
 // kernel (k_natq) moves the header windows in and out by quads of lanes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -208,7 +209,7 @@ __device__ void nat_udp_full(uint8_t* l3, int ver, int len, int l4o) {
     st16(l4p + 6, c);
 }
 
-// Descriptor checks shared by both kernels; fmt 0 entries carry IPv4 addresses only.
+// Descriptor checks shared by both kernels; fmt 0 and 2 entries carry IPv4 addresses only.
 __device__ __forceinline__ bool nat_desc_ok(uint64_t off, int len, int l4o, int ver, uint64_t arena_len, int fmt) {
     if (off > arena_len || (uint64_t)len > arena_len - off) return false;
     if (ver == 4) return len >= 20 && l4o >= 20 && l4o <= len && !(l4o & 3);
@@ -220,9 +221,16 @@ __device__ __forceinline__ bool nat_l4sum(int ver, int proto, int len, int l4o) 
     return fld >= 0 && !(ver == 4 && proto == 58) && len - l4o >= fld + 2;
 }
 
+// Packet p's descriptor and rewrite.  FMT 2 (vpcsum_nat4_rec_t): desc and rw both point at the
+// records, the descriptor is the record's first 16 B and the IPv4 entry its second.
+template <int FMT>
+__device__ __forceinline__ uint4 nat_load_desc(const uint4* desc, uint32_t p) {
+    return FMT == 2 ? desc[2 * (size_t)p] : desc[p];
+}
 template <int FMT>
 __device__ __forceinline__ NatRw nat_load_rw(const void* rw, uint32_t p) {
     if (FMT == 0) return nat_rw4(((const uint4*)rw)[p]);
+    if (FMT == 2) return nat_rw4(((const uint4*)rw)[2 * (size_t)p + 1]);
     const uint4* q = (const uint4*)rw + 3 * (size_t)p;
     return nat_rw6(q[0], q[1], q[2]);
 }
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(256) void k_nat(uint8_t* __restrict__ arena, uint64
     for (uint32_t p0 = blockIdx.x * blockDim.x; p0 < n; p0 += gridDim.x * blockDim.x) {
         const uint32_t p = p0 + threadIdx.x;
         uint32_t v = 0;
-        if (p < n) v = nat_scalar<FMT>(arena, arena_len, desc[p], nat_load_rw<FMT>(rw, p), strict != 0);
+        if (p < n) v = nat_scalar<FMT>(arena, arena_len, nat_load_desc<FMT>(desc, p), nat_load_rw<FMT>(rw, p), strict != 0);
         if (res) store_bytes_packed(res, p, n, v);
     }
 }
@@ -348,7 +356,7 @@ __global__ __launch_bounds__(256) void k_natw(uint8_t* __restrict__ arena, uint6
 #pragma unroll
         for (int i = 0; i < W; ++i) {
             const uint32_t p = p0 + i * T;
-            dv[i] = p < n ? desc[p] : make_uint4(0, 0, 0, 0);
+            dv[i] = p < n ? nat_load_desc<FMT>(desc, p) : make_uint4(0, 0, 0, 0);
             rr[i] = nat_load_rw<FMT>(rw, p < n ? p : 0);
         }
 #pragma unroll
@@ -494,7 +502,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
         for (int i = 0; i < W; ++i) {
             const uint32_t p = p0 + i * T;
-            dv[i] = p < n ? desc[p] : make_uint4(0, 0, 0, 0);
+            dv[i] = p < n ? nat_load_desc<FMT>(desc, p) : make_uint4(0, 0, 0, 0);
             rr[i] = nat_load_rw<FMT>(rw, p < n ? p : 0);
         }
         v4u v[W][4];   // quad round 0 (chunks 0..3); a second round, when a window needs it, is rare
@@ -634,7 +642,7 @@ __global__ __launch_bounds__(256) void k_nat_ttl_status(const uint8_t* __restric
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const NatRw r = nat_load_rw<FMT>(rw, p);
         if (!(r.mask & VPCSUM_NAT_DEC_TTL) || status[p] != VPCSUM_S_BAD_DESC) continue;
-        const uint4 dv = desc[p];
+        const uint4 dv = nat_load_desc<FMT>(desc, p);
         const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
         const int len = dv.z & 0xffff, l4o = dv.z >> 16, ver = dv.w & 0xff;
         if (nat_desc_ok(off, len, l4o, ver, arena_len, FMT) && nat_ttl_expired(arena + off, ver, r))
@@ -678,7 +686,7 @@ static uint32_t nat_grid(uint32_t n, int wl2, uint32_t wgs_per_cu) {
 static int nat_chunks_sel(uint32_t nat_mode, int fmt) {
     const uint32_t c = (nat_mode >> 16) & 3u;
     if (c == 1) return 6;
-    if (c == 2 && fmt == 0) return 4;
+    if (c == 2 && fmt != 1) return 4;
     return kNatChunks;
 }
 // Default: 24 workgroups per CU (4 resident at 101 VGPRs, so the grid-stride loop starts in six
@@ -700,7 +708,10 @@ hipError_t launch_nat_probe(uint8_t* arena, uint64_t arena_len, const vpcsum_des
     const uint4* d = (const uint4*)desc;
     constexpr int W = 1 << kNatWideLog2;
     if (!(tune & 0x800000u)) {   // the quad layout (k_natq), as launch_nat's default
-        if (fmt == 0 && nat_chunks_sel(tune, 0) == 4)
+        if (fmt == 2)
+            hipLaunchKernelGGL((k_natq<2, false, W, true>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n,
+                               (uint8_t*)nullptr, (uint8_t*)nullptr);
+        else if (fmt == 0 && nat_chunks_sel(tune, 0) == 4)
             hipLaunchKernelGGL((k_natq<0, false, W, true, 4>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n,
                                (uint8_t*)nullptr, (uint8_t*)nullptr);
         else if (fmt == 0)
@@ -744,7 +755,9 @@ hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d
             hipLaunchKernelGGL((k_natq<F, S, W, false, C>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out); \
     } while (0)
 #define VPC_NATQ_W(F, S, C) do { if (wl2 == 0) VPC_NATQ(F, S, 1, C); else VPC_NATQ(F, S, 2, C); } while (0)
-        if (fmt == 0 && ch == 4) {
+        if (fmt == 2) {   // records: RFC 1624 only (the strict recompute takes plain descriptors)
+            if (ch == 4) VPC_NATQ_W(2, false, 4); else VPC_NATQ_W(2, false, kNatChunks);
+        } else if (fmt == 0 && ch == 4) {
             if (strict) VPC_NATQ_W(0, true, 4); else VPC_NATQ_W(0, false, 4);
         } else if (fmt == 0) {
             if (strict) VPC_NATQ_W(0, true, kNatChunks); else VPC_NATQ_W(0, false, kNatChunks);
@@ -756,7 +769,9 @@ hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d
     } else if (wide) {
 #define VPC_NAT(F, S, W, C) hipLaunchKernelGGL((k_natw<F, S, W, false, C>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out)
 #define VPC_NAT_W(F, S) do { if (wl2 == 0) VPC_NAT(F, S, 1, kNatChunks); else if (wl2 == 1) VPC_NAT(F, S, 2, kNatChunks); else VPC_NAT(F, S, 4, kNatChunks); } while (0)
-        if (fmt == 0 && !strict && ch == 4) {
+        if (fmt == 2) {
+            VPC_NAT_W(2, false);
+        } else if (fmt == 0 && !strict && ch == 4) {
             if (wl2 == 2) VPC_NAT(0, false, 4, 4); else VPC_NAT(0, false, 2, 4);
         } else if (fmt == 0) {
             if (strict) VPC_NAT_W(0, true); else VPC_NAT_W(0, false);
@@ -765,6 +780,8 @@ hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d
         }
 #undef VPC_NAT_W
 #undef VPC_NAT
+    } else if (fmt == 2) {
+        hipLaunchKernelGGL(k_nat<2>, dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out, 0);
     } else if (fmt == 0) {
         hipLaunchKernelGGL(k_nat<0>, dim3(g), dim3(256), 0, stream, arena, arena_len, d, rw, n, status, flags_out, strict ? 1 : 0);
     } else {

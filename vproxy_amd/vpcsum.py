@@ -31,6 +31,7 @@ NAT4_DTYPE = np.dtype([("src", "u1", 4), ("dst", "u1", 4), ("sport", "u1", 2), (
                        ("mask", "u1"), ("rsv", "u1", 3)])
 NAT_DTYPE = np.dtype([("src", "u1", 16), ("dst", "u1", 16), ("sport", "u1", 2), ("dport", "u1", 2),
                       ("mask", "u1"), ("ttl", "u1"), ("rsv", "u1", 10)])
+NAT4R_DTYPE = np.dtype([("desc", DESC_DTYPE), ("rw", NAT4_DTYPE)])   # vpcsum_nat4_rec_t, 32 B
 # vpcsum_tuple_t: the flow tuple of a parsed frame (network-order addresses and ports)
 TUPLE_DTYPE = np.dtype([("src", "u1", 16), ("dst", "u1", 16), ("sport", "u1", 2), ("dport", "u1", 2),
                         ("l3_ver", "u1"), ("l4_proto", "u1"), ("tcp_flags", "u1"), ("rsv", "u1")])
@@ -40,7 +41,8 @@ EXPORTS = [
     "vpcsum_abi_version", "vpcsum_last_error", "vpcsum_device_count", "vpcsum_set_device",
     "vpcsum_compute_async", "vpcsum_nat4_async", "vpcsum_nat_async", "vpcsum_parse_ether_async",
     "vpcsum_parse_ether_tuples_async", "vpcsum_read_probe_async",
-    "vpcsum_pattern_probe_async", "vpcsum_nat4_pattern_probe_async",
+    "vpcsum_pattern_probe_async", "vpcsum_nat4_pattern_probe_async", "vpcsum_nat4r_async",
+    "vpcsum_nat4r_pattern_probe_async",
     "vpcsum_synth_async", "vpcsum_event_create", "vpcsum_event_destroy", "vpcsum_event_record",
     "vpcsum_event_elapsed_ms", "vpcsum_stream_sync", "vpcsum_ctx_create", "vpcsum_ctx_destroy",
     "vpcsum_ctx_register_arena", "vpcsum_ctx_unregister_arena", "vpcsum_ctx_submit", "vpcsum_ctx_wait",
@@ -79,6 +81,8 @@ def _declare(L):
         "vpcsum_set_device": ([I], I),
         "vpcsum_compute_async": ([P, U64, P, U32, P, P, U32, P], I),
         "vpcsum_nat4_async": ([P, U64, P, P, U32, P, U32, P], I),
+        "vpcsum_nat4r_async": ([P, U64, P, U32, P, U32, P], I),
+        "vpcsum_nat4r_pattern_probe_async": ([P, U64, P, U32, P], I),
         "vpcsum_nat_async": ([P, U64, P, P, U32, P, U32, P], I),
         "vpcsum_ctx_nat_submit": ([P, P, U64, P, P, U32, P, U32, P], I),
         "vpcsum_group_create": ([U64, U64, U32, P], I),
@@ -216,6 +220,17 @@ def pattern_probe(arena, desc, n: int, sink, grid: int = 0, stream=None):
     assert sink.numel() * sink.element_size() >= 4096, "sink needs 1024 words"
     _check(lib().vpcsum_pattern_probe_async(_ptr(arena), arena.numel(), _ptr(desc), n, _ptr(sink), grid,
                                             _stream(stream)), "vpcsum_pattern_probe_async")
+
+
+def nat4r(arena, rec, n: int, status=None, nat_mode: int = NAT_RFC1624, stream=None):
+    """vpcsum_nat4r_async: `rec` holds n NAT4R_DTYPE records (descriptor + IPv4 entry)."""
+    _check(lib().vpcsum_nat4r_async(_ptr(arena), arena.numel(), _ptr(rec), n, _ptr(status), nat_mode, _stream(stream)),
+           "vpcsum_nat4r_async")
+
+
+def nat4r_pattern_probe(arena, rec, n: int, stream=None):
+    _check(lib().vpcsum_nat4r_pattern_probe_async(_ptr(arena), arena.numel(), _ptr(rec), n, _stream(stream)),
+           "vpcsum_nat4r_pattern_probe_async")
 
 
 def nat4_pattern_probe(arena, desc, rw, n: int, stream=None):
