@@ -311,7 +311,7 @@ def test_nat_records_against_java(V, orc, pad, workload, packed):
         got, st = _gpu_nat_rec(V, arena, desc, rw, V.NAT_RFC1624 | tune)
         assert np.array_equal(st, want_st), tune
         assert np.array_equal(got, want), tune
-    with pytest.raises(V.VpcsumError, match="RFC_1624|RFC 1624"):
+    with pytest.raises(V.VpcsumError, match="RFC1624"):
         _gpu_nat_rec(V, arena, desc, rw, V.NAT_STRICT_JAVA)
 
 

@@ -80,6 +80,10 @@ fi
 if has natrec; then   # two-stream NAT vs 32-B records, and their probes, one process, interleaved
   step natrec 600 python tools/natsweep.py --rec --rounds 4
 fi
+if has trim; then   # K2 with trimmed trips (variant 80) against the default, same process, uncached batches
+  for w in c3 c2 c4; do step trim_$w 400 python tools/cold_ab.py --workload $w --teams 0,80 --batches 2 --rounds 4; done
+  step trim_c3_verify 400 python tools/cold_ab.py --workload c3 --teams 0,80 --batches 2 --rounds 4 --mode 1
+fi
 if has ab; then   # this tree's library against vproxy_amd/libvpcsum_ab.so, uncached batches, compute + verify
   step ab 1100 bash tools/ab_libs_cold.sh ${TAG}_ab "${AB_WS:-c1 c3 c2}" ${AB_ROUNDS:-2} "${AB_MODES:-0 1}"
 fi

@@ -448,8 +448,11 @@ __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, ui
 }
 
 // One team of TEAM lanes streams the packet of slot sidx (act: the team has one) and leaves its
-// {l4, ip, pseudo, stored} sums in the slot's q0.
-template <int TEAM, int U, bool VERIFY, bool NT>
+// {l4, ip, pseudo, stored} sums in the slot's q0.  TRIM: when no fast-class team of the wave needs
+// more than TEAM x (U - 1) chunks, the trip takes U - 1 loads per lane (a wave-uniform branch once
+// per iteration, not per load): C3's 576-B packets are 36 chunks, and a 48-chunk trip leaves a
+// quarter of its load slots dead -- each still an address the TA unit has to process.
+template <int TEAM, int U, bool VERIFY, bool NT, bool TRIM = false>
 __device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uint4 (*slots)[4], int tl, int sidx,
                                           bool act) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -466,7 +469,11 @@ __device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uin
     uint32_t h_l4 = 0, h_ip = 0;   // fast class: halfword sums
     if (a.y >> 31) {
         const uint4 bm = sl[1];
-        fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip, (uint16_t*)&sl[3].w);
+        if (TRIM && U > 1 && __ballot(nch > TEAM * (U - 1)) == 0)
+            fast_trips<TEAM, (U > 1 ? U - 1 : 1), VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip,
+                                                              (uint16_t*)&sl[3].w);
+        else
+            fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip, (uint16_t*)&sl[3].w);
     } else if (nch > 0) {
         const uint4 q2 = sl[2], q3 = sl[3];
         PktPlan pl;
@@ -508,7 +515,7 @@ __device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uin
 // packets per iteration.  WT: a last iteration that fills at most half of its teams (the tail of
 // the tier's costliest class, in a size-sorted unit) runs with teams of 2 x TEAM lanes, so its
 // packets need half the trips.
-template <int TEAM, int U, bool VERIFY, bool NT, bool SLOTROT = false, bool WT = false>
+template <int TEAM, int U, bool VERIFY, bool NT, bool SLOTROT = false, bool WT = false, bool TRIM = false>
 __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, uint4 (*slots)[4], int lane,
                                             int s_begin, int s_end, uint32_t rot = 0) {
     constexpr int PPI = 64 / TEAM;
@@ -534,7 +541,7 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
             sidx = s_begin + (it + r0 < nit ? it + r0 : it + r0 - nit) * PPI + tid;
             act = sidx < s_end;
         }
-        tier_team<TEAM, U, VERIFY, NT>(rsrc, slots, tl, sidx, act);
+        tier_team<TEAM, U, VERIFY, NT, TRIM>(rsrc, slots, tl, sidx, act);
     }
     if (WT && TEAM <= 16 && wide) {
         constexpr int T2 = TEAM <= 16 ? 2 * TEAM : TEAM;
@@ -650,7 +657,7 @@ __device__ __forceinline__ void store_result(uint32_t* out, uint8_t* status, uin
 // k_csum_service: the persistent service grid, once per batch).
 // ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
 // ROT > 0 rotates whole iterations (64 / TEAM packets), ROT < 0 single slots.
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool TRIM = false>
 __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -1028,7 +1035,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         // ---- phase B: teams stream the packets in slot order ----
         if (TS > 0) {
             stream_tier<(TS > 0 ? TS : 1), US, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, n_small);
-            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0), WT>(rsrc, s_slot[wid], lane, n_small, 64,
+            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0), WT, TRIM>(rsrc, s_slot[wid], lane, n_small, 64,
                                              // rotated only when the tier is one cost class: in a
                                              // sorted mixed tier the wrap would pair unlike sizes
                                              (ROT && n_cls == 1) ? (blk * 4u + (uint32_t)wid) * (uint32_t)(ROT < 0 ? -ROT : ROT) : 0u);
@@ -1067,13 +1074,13 @@ constexpr int k2_waves_per_eu() {
                          : 1;
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool TRIM = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_per_eu<TEAM, U, TS, US, VERIFY, WPE, IL, ROT, SF, WT, DS>()))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
                                                 uint8_t* __restrict__ arena_w, uint32_t low_grid) {
-    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS>(arena, arena_len, desc, n, out, status, flags_override, arena_w,
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS, TRIM>(arena, arena_len, desc, n, out, status, flags_override, arena_w,
                                                 low_grid, blockIdx.x, gridDim.x);
 }
 
@@ -1293,7 +1300,7 @@ static uint32_t default_low_grid() {
     return (uint32_t)num_cus(dev) * 2u;
 }
 
-template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool TRIM = false>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, bool adapt, hipStream_t stream) {
@@ -1316,7 +1323,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     const uint32_t cus = (uint32_t)num_cus(dev);
 #define VPC_LAUNCH(V, N)                                                                                         \
     do {                                                                                                         \
-        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT, DS>;                                       \
+        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT, DS, TRIM>;                                 \
         uint32_t gg = g;                                                                                         \
         if (dense) {                                                                                             \
             static const uint32_t res = resident_wgs((const void*)kern);                                         \
@@ -1383,6 +1390,9 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 76: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         // 78: the team kernel with 64-bit loads, which serves arenas past 4 GiB (A/B, tooling)
         case 78: return launch_team<kDefaultTeam, kDefaultUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid > 0 ? grid : (int)default_grid(), stream);
+        // 80 / 81: the default's staged / unstaged build with trimmed trips (TRIM, A/B)
+        case 80: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        case 81: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         // 79: the staging build on every batch (round 3's r03w default, A/B)
         case 79: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 70:
