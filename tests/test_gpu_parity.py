@@ -1153,6 +1153,59 @@ def test_batches_straddling_4gib(V, orc):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("order", ["sorted", "reversed", "two_swapped"])
+def test_windowed_k2_past_4gib(V, orc, order):
+    """The default launcher on a 9-GiB arena runs K2 once per 2-GiB window (kernels.hip kWinBytes):
+    dense 64-B frames straddling the 2-GiB and 4-GiB window lines, C2 frames in the fourth window,
+    mixed FUZZ frames at the arena's end (the window [8, 9) GiB is cut short by the arena end).  Sorted descriptors go to their
+    windows' launches; reversed ones and a batch with two descriptors swapped across windows leave
+    packets to the leftover pass (k_win_left).  Compute, verify and write-back equal the oracle."""
+    import torch
+    pieces = []   # (synth id, packets, stride, pad, arena offset)
+    pieces.append((O.SYNTH_C1, 3000, 64, 14, (2 << 30) - 64 * 1500))
+    pieces.append((O.SYNTH_C1, 3000, 64, 14, (4 << 30) - 64 * 1500))
+    pieces.append((O.SYNTH_C2, 600, 2048, 0, (6 << 30) + 12345 * 16))
+    pieces.append((O.SYNTH_FUZZ, 300, 9216, 6, (9 << 30) - 300 * 9216 - 4096))
+    big = torch.zeros((9 << 30) + 64, dtype=torch.uint8, device="cuda")
+    arrs, descs, wants = [], [], []
+    for k, (sid, m, stride, pad, base) in enumerate(pieces):
+        a, d = orc.synth(m, stride, pad, sid, O.SEED, 1000 * k)
+        w, _ = orc.process(a, d, O.MODE_COMPUTE)
+        big[base:base + len(a)] = torch.from_numpy(a).cuda()
+        dg = d.copy()
+        dg["l3_off"] += base
+        arrs.append((base, a, d))
+        descs.append(dg)
+        wants.append(w)
+    dall, want = np.concatenate(descs), np.concatenate(wants)
+    perm = np.arange(len(dall))
+    if order == "reversed":
+        perm = perm[::-1].copy()
+    elif order == "two_swapped":
+        perm[[10, len(perm) - 10]] = perm[[len(perm) - 10, 10]]
+    dall, want = dall[perm], want[perm]
+    n = len(dall)
+    dt = V.desc_to_tensor(dall)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    V.compute(big, dt, n, out, st, O.MODE_COMPUTE)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    assert np.all(st.cpu().numpy() == O.S_DONE)
+    V.compute(big, dt, n, out, None, O.MODE_WRITE)
+    V.compute(big, dt, n, None, st, O.MODE_VERIFY)
+    torch.cuda.synchronize()
+    stn = st.cpu().numpy()
+    want_ok = np.where(dall["flags"] & 1, 1, 0) | np.where(dall["flags"] & 2, 2, 0)
+    assert np.array_equal(stn & 3, want_ok)
+    for base, a, d in arrs:
+        a2 = a.copy()
+        orc.process(a2, d, O.MODE_COMPUTE, write=True)
+        assert np.array_equal(big[base:base + len(a)].cpu().numpy(), a2)
+    del big
+    torch.cuda.empty_cache()
+
+
 def test_parse_rules_on_gpu(V, orc):
     """k_parse_ether and ctx_verify_frames against the oracle's parse on frames at every edge of
     the reference's parse rules (tests/edgevec.py:parse_cases): TCP under 20 B, UDP under 8 B,

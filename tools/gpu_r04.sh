@@ -84,6 +84,9 @@ if has trim; then   # K2 with trimmed trips (variant 80) against the default, sa
   for w in c3 c2 c4; do step trim_$w 400 python tools/cold_ab.py --workload $w --teams 0,80 --batches 2 --rounds 4; done
   step trim_c3_verify 400 python tools/cold_ab.py --workload c3 --teams 0,80 --batches 2 --rounds 4 --mode 1
 fi
+if has bigarena; then   # arenas past 4 GiB: windowed K2 vs views under 4 GiB vs the team kernel
+  step bigarena 600 python tools/big_arena.py
+fi
 if has ab; then   # this tree's library against vproxy_amd/libvpcsum_ab.so, uncached batches, compute + verify
   step ab 1100 bash tools/ab_libs_cold.sh ${TAG}_ab "${AB_WS:-c1 c3 c2}" ${AB_ROUNDS:-2} "${AB_MODES:-0 1}"
 fi

@@ -653,16 +653,34 @@ __device__ __forceinline__ void store_result(uint32_t* out, uint8_t* status, uin
     }
 }
 
+// Arenas past 4 GiB.  K2 addresses frames with 32-bit buffer offsets, so the launcher cuts such an
+// arena into windows of kWinBytes (each launch's buffer covers its window plus the 64 KiB the
+// largest packet starting in it can reach, under 4 GiB) and launches K2 once per window, over the
+// descriptor range [lo_w, hi_w) a k-ary search found for the window's offsets (k_win_split; for
+// address-sorted descriptors, the packets that start in it).  A packet of that range that does
+// not start in the window (unsorted descriptors) is counted and left to k_win_left, which runs the
+// team kernel's 64-bit path over exactly those packets -- and returns at once when the count is 0.
+constexpr uint64_t kWinBytes = 1ull << 31;
+constexpr uint64_t kWinSpan = kWinBytes + 65536;
+constexpr uint32_t kMaxWin = 256;   // arenas up to 512 GiB take windows
+struct WinArg {
+    uint64_t base;           // the window's first arena byte (descriptor offsets are rebased by it)
+    const uint32_t* rng;     // k_win_split's boundaries rng[0..nw]; window w: [max rng[..w], max rng[..w+1])
+    uint32_t* left;          // packets of the window's range that start outside it
+    uint32_t w;
+};
+
 // K2 body for workgroup `blk` of a grid of `gdim` workgroups (k_csum_d: the launch grid;
 // k_csum_service: the persistent service grid, once per batch).
 // ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
 // ROT > 0 rotates whole iterations (64 / TEAM packets), ROT < 0 single slots.
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool TRIM = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool TRIM = false, bool WIN = false>
 __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                        const uint8_t* __restrict__ flags_override,
-                                       uint8_t* __restrict__ arena_w, uint32_t low_grid, uint32_t blk, uint32_t gdim) {
+                                       uint8_t* __restrict__ arena_w, uint32_t low_grid, uint32_t blk, uint32_t gdim,
+                                       const WinArg win = WinArg{0, nullptr, nullptr, 0}) {
     // slot: q0 {boff, nch | klo<<16 | do_ip<<30 | fast<<31, kfast, l4hi}, q1 bitmaps,
     // q2/q3 the byte-range plan of the slow class; q0 is overwritten with the team's sums.
     __shared__ uint4 s_slot[4][64][4];
@@ -685,7 +703,20 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     // Workgroups below low_grid work in either case and fetch their first descriptors before
     // the sample, so the two loads overlap.
     uint32_t grid = gdim;
-    uint32_t P0 = IL == 1 ? blk * 256u : ((blk * 256u + threadIdx.x) >> 6) * 64u;
+    // WIN: this launch covers packets [base_p, n) of the batch, its window's descriptor range
+    uint32_t base_p = 0;
+    if (WIN) {
+        uint32_t a = 0, b = 0;
+        for (uint32_t k = 0; k <= win.w + 1; ++k) {
+            const uint32_t r = win.rng[k];
+            if (k <= win.w) a = max(a, r);
+            b = max(b, r);
+        }
+        base_p = a;
+        n = min(b, n);
+        if (n <= base_p) return;   // an empty window: the whole workgroup, before any LDS use
+    }
+    uint32_t P0 = base_p + (IL == 1 ? blk * 256u : ((blk * 256u + threadIdx.x) >> 6) * 64u);
     uint4 dnext = make_uint4(0, 0, 0, 0);
     int fnext = 0;
     const bool sample = low_grid != 0 && grid > low_grid;
@@ -695,7 +726,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         if (flags_override) fnext = flags_override[P0 + lo];
     }
     if (sample) {
-        const uint4 sd = desc[(uint32_t)(((uint64_t)n * (uint32_t)lane) >> 6)];
+        const uint4 sd = desc[base_p + (uint32_t)(((uint64_t)(n - base_p) * (uint32_t)lane) >> 6)];
         if (__ballot((sd.z & 0xffffu) >= 1024u) == ~0ull) grid = low_grid;
         if (blk >= grid) return;   // whole workgroup, before any LDS use
         if (!early && P0 + lo < n) {
@@ -714,7 +745,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     // stream of packet reads once per unit.  Other batches (small and
     // mixed packets: short-lived waves, nothing to batch) and waves of fewer than 4 units (C4's
     // 2 per wave: -0.3%) store each unit's words at once.
-    const bool stage = DS && grid < gdim && n / 4u >= wstride;
+    const bool stage = DS && grid < gdim && (n - base_p) / 4u >= wstride;
     __shared__ uint32_t s_eo[4][DS ? kEsUnits : 1][64];
     __shared__ uint8_t s_es[4][DS ? kEsUnits : 1][64];
     uint32_t es_n = 0, es_P0 = P0;
@@ -747,8 +778,15 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                 if (flags_override) fnext = flags_override[q];
             }
         }
-        const bool live = P0 + lo < n;
-        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        bool live = P0 + lo < n;
+        uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        if (WIN) {   // a packet that does not start in this window goes to k_win_left
+            const bool inw = off >= win.base && off - win.base < kWinBytes;
+            const uint64_t m = __ballot(live && !inw);
+            if (m != 0 && lane == 0) atomicAdd(win.left, (uint32_t)__popcll(m));
+            live = live && inw;
+            off -= win.base;
+        }
         const int len = dv.z & 0xffff;
         const int l4o = dv.z >> 16;
         const int ver = dv.w & 0xff;
@@ -1074,14 +1112,89 @@ constexpr int k2_waves_per_eu() {
                          : 1;
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool TRIM = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool TRIM = false, bool WIN = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_per_eu<TEAM, U, TS, US, VERIFY, WPE, IL, ROT, SF, WT, DS>()))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
-                                                uint8_t* __restrict__ arena_w, uint32_t low_grid) {
-    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS, TRIM>(arena, arena_len, desc, n, out, status, flags_override, arena_w,
-                                                low_grid, blockIdx.x, gridDim.x);
+                                                uint8_t* __restrict__ arena_w, uint32_t low_grid, WinArg win) {
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS, TRIM, WIN>(arena, arena_len, desc, n, out, status, flags_override,
+                                                                       arena_w, low_grid, blockIdx.x, gridDim.x, win);
+}
+
+// Window boundaries (arenas past 4 GiB): block w in 1..nw-1 finds the first descriptor whose offset
+// is at least w x kWinBytes with a 256-way search (each round narrows the range 256-fold: 4 rounds
+// for 16M packets, a dependent load each); block 0 writes 0 and clears the leftover count, block nw
+// writes n.  Unsorted descriptors give some index: the launches take prefix maxima, so the ranges
+// still partition the batch.
+__global__ __launch_bounds__(256) void k_win_split(const uint4* __restrict__ desc, uint32_t n, uint32_t nw,
+                                                   uint32_t* __restrict__ rng, uint32_t* __restrict__ left) {
+    const uint32_t w = blockIdx.x;
+    if (w == 0 || w == nw) {
+        if (threadIdx.x == 0) {
+            rng[w] = w == 0 ? 0u : n;
+            if (w == 0) *left = 0u;
+        }
+        return;
+    }
+    const uint64_t target = (uint64_t)w * kWinBytes;
+    __shared__ uint32_t s_first;
+    uint32_t lo = 0, hi = n;   // the answer lies in [lo, hi]; hi: no descriptor of [lo, hi) qualifies
+    while (lo < hi) {
+        const uint32_t sz = hi - lo;
+        const uint32_t idx = lo + (uint32_t)(((uint64_t)sz * threadIdx.x) >> 8);
+        const uint4 d = desc[idx];
+        const bool pred = ((uint64_t)d.x | ((uint64_t)d.y << 32)) >= target;
+        if (threadIdx.x == 0) s_first = 256u;
+        __syncthreads();
+        if (pred) atomicMin(&s_first, threadIdx.x);
+        __syncthreads();
+        const uint32_t j = s_first;
+        __syncthreads();
+        if (j == 0) {
+            hi = lo;
+        } else {
+            const uint32_t prev = lo + (uint32_t)(((uint64_t)sz * (j - 1)) >> 8);
+            hi = j < 256u ? lo + (uint32_t)(((uint64_t)sz * j) >> 8) : hi;
+            lo = prev + 1;
+        }
+    }
+    if (threadIdx.x == 0) rng[w] = lo;
+}
+
+// The packets the window launches left (see kWinBytes): teams of 8 lanes walk the batch and take
+// each packet whose offset lies outside the window its index fell to, through the team kernel's
+// 64-bit path (k1_packet).  Nothing to do (address-sorted descriptors): one load, then return.
+template <bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) void k_win_left(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                  const uint4* __restrict__ desc, uint32_t n,
+                                                  uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                                  const uint8_t* __restrict__ flags_override,
+                                                  uint8_t* __restrict__ arena_w, const uint32_t* __restrict__ rng,
+                                                  uint32_t nw, const uint32_t* __restrict__ left) {
+    if (*left == 0u) return;
+    __shared__ uint32_t s_lo[kMaxWin + 1];
+    for (uint32_t k = threadIdx.x; k <= nw; k += blockDim.x) s_lo[k] = rng[k];
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (uint32_t k = 1; k <= nw; ++k) s_lo[k] = max(s_lo[k], s_lo[k - 1]);
+    __syncthreads();
+    constexpr int TEAM = kDefaultTeam;
+    const int tl = threadIdx.x & (TEAM - 1);
+    const uint32_t nteams = gridDim.x * (256u / TEAM);
+    for (uint32_t p = (blockIdx.x * 256u + threadIdx.x) / TEAM; p < n; p += nteams) {
+        uint32_t a = 0, b = nw;   // the window of index p: the last w with s_lo[w] <= p
+        while (b - a > 1) {
+            const uint32_t m = (a + b) >> 1;
+            if (s_lo[m] <= p) a = m; else b = m;
+        }
+        const uint4 dv = desc[p];
+        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        const uint64_t base = (uint64_t)a * kWinBytes;
+        if (off >= base && off - base < kWinBytes) continue;   // its window launch took it
+        k1_packet<TEAM, kDefaultUnroll, VERIFY, NT>(arena, arena_len, dv, flags_override ? flags_override[p] : 0,
+                                                    flags_override != nullptr, p, out, status, arena_w, tl);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1332,7 +1445,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
         if (gg > need) gg = need;                                                                                \
         if (gg == 0) gg = 1;                                                                                     \
         hipLaunchKernelGGL(kern, dim3(gg), dim3(256), 0, stream, arena, arena_len, (const uint4*)desc, n, out,   \
-                           status, flags_override, arena_w, low_grid);                                            \
+                           status, flags_override, arena_w, low_grid, WinArg{0, nullptr, nullptr, 0});            \
     } while (0)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -1341,6 +1454,57 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     }
 #undef VPC_LAUNCH
     return hipGetLastError();
+}
+
+// The default K2 over an arena past 4 GiB (see kWinBytes): the window boundaries, one K2 launch per
+// window (the sampled low grid and the dense grid decided on the whole batch, as for a smaller
+// arena), and the leftover pass, all on `stream`; the boundaries live in stream-ordered scratch.
+template <bool DS>
+static hipError_t launch_dw(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
+                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
+                            uint8_t* arena_w, bool adapt, hipStream_t stream) {
+    const uint32_t nw = (uint32_t)((arena_len + kWinBytes - 1) / kWinBytes);
+    uint32_t* ctl = nullptr;
+    hipError_t e = hipMallocAsync((void**)&ctl, (size_t)(nw + 2) * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    uint32_t* rng = ctl;
+    uint32_t* left = ctl + nw + 1;
+    hipLaunchKernelGGL(k_win_split, dim3(nw + 1), dim3(256), 0, stream, (const uint4*)desc, n, nw, rng, left);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint32_t cus = (uint32_t)num_cus(dev);
+    const uint32_t low_grid = (!adapt || arena_len < (uint64_t)n * 1024u) ? 0u : default_low_grid();
+    const bool dense = adapt && arena_len <= (uint64_t)n * 128u;
+    const uint32_t need = (n + 255) / 256;
+#define VPC_LAUNCH_W(V, N)                                                                                        \
+    do {                                                                                                          \
+        auto kern = k_csum_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, V, N, 1, 0, kDefaultRot, true,  \
+                             false, DS, false, true>;                                                             \
+        uint32_t gg = default_grid();                                                                             \
+        if (dense) {                                                                                              \
+            static const uint32_t res = resident_wgs((const void*)kern);                                          \
+            gg = min(gg, res * cus);                                                                              \
+        }                                                                                                         \
+        gg = max(1u, min(gg, need));                                                                              \
+        for (uint32_t w = 0; w < nw; ++w) {                                                                       \
+            const uint64_t base = (uint64_t)w * kWinBytes;                                                        \
+            const uint64_t len = min(kWinSpan, arena_len - base);                                                 \
+            hipLaunchKernelGGL(kern, dim3(gg), dim3(256), 0, stream, arena + base, len, (const uint4*)desc, n, out, \
+                               status, flags_override, arena_w ? arena_w + base : nullptr, low_grid,               \
+                               WinArg{base, rng, left, w});                                                       \
+        }                                                                                                         \
+        hipLaunchKernelGGL((k_win_left<V, N>), dim3(cus * 8u), dim3(256), 0, stream, arena, arena_len,            \
+                           (const uint4*)desc, n, out, status, flags_override, arena_w, rng, nw, left);           \
+    } while (0)
+    if (verify) {
+        if (nt) VPC_LAUNCH_W(true, true); else VPC_LAUNCH_W(true, false);
+    } else {
+        if (nt) VPC_LAUNCH_W(false, true); else VPC_LAUNCH_W(false, false);
+    }
+#undef VPC_LAUNCH_W
+    e = hipGetLastError();
+    const hipError_t ef = hipFreeAsync(ctl, stream);
+    return e != hipSuccess ? e : ef;
 }
 
 hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
@@ -1397,9 +1561,16 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 79: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 70:
         case 0:
+            // Arenas past 4 GiB: K2 per 2-GiB window (see kWinBytes) -- larger than any window
+            // table, or not 16-B aligned: the team kernel (launch_d's fallback)
+            if (grid <= 0 && arena_len > kMaxBufArena && !((uintptr_t)arena & 15) &&
+                arena_len <= (uint64_t)kMaxWin * kWinBytes) {
+                if (adapt && arena_len <= (uint64_t)n * 128u)
+                    return launch_dw<false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, adapt, stream);
+                return launch_dw<true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, adapt, stream);
+            }
             // Dense small frames (at most 128 arena bytes per packet: C1) never stage their result
-            // words, and the staging build holds 92 VGPRs against 79 (5 resident waves per SIMD
-            // instead of 6): they take the build without staging
+            // words: they take the build without staging and its smaller LDS
             if (grid <= 0 && adapt && arena_len <= (uint64_t)n * 128u)
                 return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
             return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
