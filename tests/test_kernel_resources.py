@@ -55,11 +55,11 @@ def pick(ks: dict, pattern: str) -> dict:
 
 def test_k2_default_builds_budgets():
     ks = kernels("kernels.hip.o")
-    # k_csum_d<8, 6, 2, 2, VERIFY, NT, 1, 0, -9, true, false, DS, TRIM = false, WIN>: the default
-    # builds, and their window builds for arenas past 4 GiB (WIN)
-    unstaged_compute = pick(ks, r"k_csum_dILi8ELi6ELi2ELi2ELb0ELb[01]ELi1ELi0ELin9ELb1ELb0ELb0ELb0ELb[01]E")
-    staged_compute = pick(ks, r"k_csum_dILi8ELi6ELi2ELi2ELb0ELb[01]ELi1ELi0ELin9ELb1ELb0ELb1ELb0ELb[01]E")
-    verify = pick(ks, r"k_csum_dILi8ELi6ELi2ELi2ELb1ELb[01]ELi1ELi0ELin9ELb1ELb0ELb[01]ELb0ELb[01]E")
+    # k_csum_d<8, 6, 2, 2, VERIFY, NT, 1, 0, -9, true, false, DS, WIN>: the default builds, and
+    # their window builds for arenas past 4 GiB (WIN)
+    unstaged_compute = pick(ks, r"k_csum_dILi8ELi6ELi2ELi2ELb0ELb[01]ELi1ELi0ELin9ELb1ELb0ELb0ELb[01]E")
+    staged_compute = pick(ks, r"k_csum_dILi8ELi6ELi2ELi2ELb0ELb[01]ELi1ELi0ELin9ELb1ELb0ELb1ELb[01]E")
+    verify = pick(ks, r"k_csum_dILi8ELi6ELi2ELi2ELb1ELb[01]ELi1ELi0ELin9ELb1ELb0ELb[01]ELb[01]E")
     assert len(unstaged_compute) == len(staged_compute) == 4 and len(verify) == 8
     # every default build fits 6 waves per SIMD (the verify and staging builds since round 4:
     # stored fields loaded in phase A, a scalar wave index, opaque result-store indices)
@@ -75,12 +75,11 @@ def test_k2_default_builds_budgets():
 def test_no_scratch_in_default_kernels():
     ks = {**kernels("kernels.hip.o"), **kernels("nat.hip.o")}
     # the NAT kernels at their default occupancy (k_natq ... WPE 1), the byte kernel, the lane
-    # layout, parse, service, probes, the window kernels; the forced-occupancy tuning shapes (WPE
-    # 6 / 8) and the trimmed-trip A/B variants of K2 (TRIM) may spill
+    # layout, parse, service, probes, every K2 build (the window builds included); the
+    # forced-occupancy tuning shapes (WPE 6 / 8) may spill
     default = {k: v for k, v in ks.items()
                if re.search(r"k_natq\w*ELi1EEEv|k_natw|k_natILi|k_parse_ether|k_csum_service|k_pattern_probe|k_read_probe|"
-                            r"k_win_|k_csum_d", k)
-               and not re.search(r"k_csum_dILi8ELi6ELi2ELi2ELb[01]ELb[01]ELi1ELi0ELin9ELb1ELb0ELb[01]ELb1E", k)}
+                            r"k_csum_d", k)}
     assert len(default) > 20
     spills = {k: v["private_segment_fixed_size"] for k, v in default.items() if v["private_segment_fixed_size"]}
     assert not spills, spills

@@ -80,10 +80,6 @@ fi
 if has natrec; then   # two-stream NAT vs 32-B records, and their probes, one process, interleaved
   step natrec 600 python tools/natsweep.py --rec --rounds 4
 fi
-if has trim; then   # K2 with trimmed trips (variant 80) against the default, same process, uncached batches
-  for w in c3 c2 c4; do step trim_$w 400 python tools/cold_ab.py --workload $w --teams 0,80 --batches 2 --rounds 4; done
-  step trim_c3_verify 400 python tools/cold_ab.py --workload c3 --teams 0,80 --batches 2 --rounds 4 --mode 1
-fi
 if has bigarena; then   # arenas past 4 GiB: windowed K2 vs views under 4 GiB vs the team kernel
   step bigarena 600 python tools/big_arena.py
 fi

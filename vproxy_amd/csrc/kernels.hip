@@ -448,11 +448,8 @@ __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, ui
 }
 
 // One team of TEAM lanes streams the packet of slot sidx (act: the team has one) and leaves its
-// {l4, ip, pseudo, stored} sums in the slot's q0.  TRIM: when no fast-class team of the wave needs
-// more than TEAM x (U - 1) chunks, the trip takes U - 1 loads per lane (a wave-uniform branch once
-// per iteration, not per load): C3's 576-B packets are 36 chunks, and a 48-chunk trip leaves a
-// quarter of its load slots dead -- each still an address the TA unit has to process.
-template <int TEAM, int U, bool VERIFY, bool NT, bool TRIM = false>
+// {l4, ip, pseudo, stored} sums in the slot's q0.
+template <int TEAM, int U, bool VERIFY, bool NT>
 __device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uint4 (*slots)[4], int tl, int sidx,
                                           bool act) {
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -469,11 +466,7 @@ __device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uin
     uint32_t h_l4 = 0, h_ip = 0;   // fast class: halfword sums
     if (a.y >> 31) {
         const uint4 bm = sl[1];
-        if (TRIM && U > 1 && __ballot(nch > TEAM * (U - 1)) == 0)
-            fast_trips<TEAM, (U > 1 ? U - 1 : 1), VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip,
-                                                              (uint16_t*)&sl[3].w);
-        else
-            fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip, (uint16_t*)&sl[3].w);
+        fast_trips<TEAM, U, VERIFY, NT>(rsrc, boff, nch, klo, kfast, l4hi, bm, tl, h_l4, h_ip, (uint16_t*)&sl[3].w);
     } else if (nch > 0) {
         const uint4 q2 = sl[2], q3 = sl[3];
         PktPlan pl;
@@ -515,7 +508,7 @@ __device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uin
 // packets per iteration.  WT: a last iteration that fills at most half of its teams (the tail of
 // the tier's costliest class, in a size-sorted unit) runs with teams of 2 x TEAM lanes, so its
 // packets need half the trips.
-template <int TEAM, int U, bool VERIFY, bool NT, bool SLOTROT = false, bool WT = false, bool TRIM = false>
+template <int TEAM, int U, bool VERIFY, bool NT, bool SLOTROT = false, bool WT = false>
 __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, uint4 (*slots)[4], int lane,
                                             int s_begin, int s_end, uint32_t rot = 0) {
     constexpr int PPI = 64 / TEAM;
@@ -541,7 +534,7 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
             sidx = s_begin + (it + r0 < nit ? it + r0 : it + r0 - nit) * PPI + tid;
             act = sidx < s_end;
         }
-        tier_team<TEAM, U, VERIFY, NT, TRIM>(rsrc, slots, tl, sidx, act);
+        tier_team<TEAM, U, VERIFY, NT>(rsrc, slots, tl, sidx, act);
     }
     if (WT && TEAM <= 16 && wide) {
         constexpr int T2 = TEAM <= 16 ? 2 * TEAM : TEAM;
@@ -653,39 +646,33 @@ __device__ __forceinline__ void store_result(uint32_t* out, uint8_t* status, uin
     }
 }
 
-// Arenas past 4 GiB.  K2 addresses frames with 32-bit buffer offsets, so the launcher cuts such an
-// arena into windows of kWinBytes (each launch's buffer covers its window plus the 64 KiB the
-// largest packet starting in it can reach, under 4 GiB) and launches K2 once per window, over the
-// descriptor range [lo_w, hi_w) a k-ary search found for the window's offsets (k_win_split; for
-// address-sorted descriptors, the packets that start in it).  A packet of that range that does
-// not start in the window (unsorted descriptors) is counted and left to k_win_left, which runs the
-// team kernel's 64-bit path over exactly those packets -- and returns at once when the count is 0.
+// Arenas past 4 GiB (WIN).  K2 addresses frames with 32-bit buffer offsets on one buffer resource,
+// so over a larger arena a unit takes the 2-GiB window its first packet starts in: the resource is
+// rebuilt per unit for that window (base arena + w x kWinBytes, covering the window plus the 64 KiB
+// the largest packet starting in it can reach), and the unit's packets that start elsewhere are
+// done afterwards one at a time by the whole wave through the team kernel's 64-bit loads
+// (k1_packet, 64 lanes).  Address-sorted batches (an umem's descriptors in frame order) leave such
+// packets only in the units that straddle a window line; any order is correct.
 constexpr uint64_t kWinBytes = 1ull << 31;
 constexpr uint64_t kWinSpan = kWinBytes + 65536;
-constexpr uint32_t kMaxWin = 256;   // arenas up to 512 GiB take windows
-struct WinArg {
-    uint64_t base;           // the window's first arena byte (descriptor offsets are rebased by it)
-    const uint32_t* rng;     // k_win_split's boundaries rng[0..nw]; window w: [max rng[..w], max rng[..w+1])
-    uint32_t* left;          // packets of the window's range that start outside it
-    uint32_t w;
-};
 
 // K2 body for workgroup `blk` of a grid of `gdim` workgroups (k_csum_d: the launch grid;
 // k_csum_service: the persistent service grid, once per batch).
 // ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
 // ROT > 0 rotates whole iterations (64 / TEAM packets), ROT < 0 single slots.
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool TRIM = false, bool WIN = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false>
 __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                        const uint8_t* __restrict__ flags_override,
-                                       uint8_t* __restrict__ arena_w, uint32_t low_grid, uint32_t blk, uint32_t gdim,
-                                       const WinArg win = WinArg{0, nullptr, nullptr, 0}) {
+                                       uint8_t* __restrict__ arena_w, uint32_t low_grid, uint32_t blk, uint32_t gdim) {
     // slot: q0 {boff, nch | klo<<16 | do_ip<<30 | fast<<31, kfast, l4hi}, q1 bitmaps,
     // q2/q3 the byte-range plan of the slow class; q0 is overwritten with the team's sums.
     __shared__ uint4 s_slot[4][64][4];
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, (int)buf_records(arena_len), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrc_all =
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, 0, WIN ? 0 : (int)buf_records(arena_len), 0x00020000);
+    const uint64_t arena_len_all = arena_len;
+    uint8_t* const arena_w_all = arena_w;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: an SGPR
     // packet of this lane = P0 + lo.  IL = 0: a wave owns 64 consecutive packets.  IL = 1: the 4
@@ -703,20 +690,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     // Workgroups below low_grid work in either case and fetch their first descriptors before
     // the sample, so the two loads overlap.
     uint32_t grid = gdim;
-    // WIN: this launch covers packets [base_p, n) of the batch, its window's descriptor range
-    uint32_t base_p = 0;
-    if (WIN) {
-        uint32_t a = 0, b = 0;
-        for (uint32_t k = 0; k <= win.w + 1; ++k) {
-            const uint32_t r = win.rng[k];
-            if (k <= win.w) a = max(a, r);
-            b = max(b, r);
-        }
-        base_p = a;
-        n = min(b, n);
-        if (n <= base_p) return;   // an empty window: the whole workgroup, before any LDS use
-    }
-    uint32_t P0 = base_p + (IL == 1 ? blk * 256u : ((blk * 256u + threadIdx.x) >> 6) * 64u);
+    uint32_t P0 = IL == 1 ? blk * 256u : (blk * 4u + (uint32_t)wid) * 64u;   // wave-uniform: SGPRs
     uint4 dnext = make_uint4(0, 0, 0, 0);
     int fnext = 0;
     const bool sample = low_grid != 0 && grid > low_grid;
@@ -726,7 +700,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         if (flags_override) fnext = flags_override[P0 + lo];
     }
     if (sample) {
-        const uint4 sd = desc[base_p + (uint32_t)(((uint64_t)(n - base_p) * (uint32_t)lane) >> 6)];
+        const uint4 sd = desc[(uint32_t)(((uint64_t)n * (uint32_t)lane) >> 6)];
         if (__ballot((sd.z & 0xffffu) >= 1024u) == ~0ull) grid = low_grid;
         if (blk >= grid) return;   // whole workgroup, before any LDS use
         if (!early && P0 + lo < n) {
@@ -745,22 +719,24 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     // stream of packet reads once per unit.  Other batches (small and
     // mixed packets: short-lived waves, nothing to batch) and waves of fewer than 4 units (C4's
     // 2 per wave: -0.3%) store each unit's words at once.
-    const bool stage = DS && grid < gdim && (n - base_p) / 4u >= wstride;
+    const bool stage = DS && grid < gdim && n / 4u >= wstride;
     __shared__ uint32_t s_eo[4][DS ? kEsUnits : 1][64];
     __shared__ uint8_t s_es[4][DS ? kEsUnits : 1][64];
     uint32_t es_n = 0, es_P0 = P0;
     auto es_flush = [&]() {
-        uint32_t ln = lo;
-        asm volatile("" : "+v"(ln));
+        // packet index and LDS lane through opaque copies: the addresses are the same for every
+        // flush, and hoisted out of the unit loop they would be kept live (or spilled) across it
+        uint32_t ln = lo, la = (uint32_t)lane;
+        asm volatile("" : "+v"(ln), "+v"(la));
         for (uint32_t k = 0; k < es_n; ++k) {
             const uint32_t p = es_P0 + k * wstride + ln;
             if (p < n) {
                 if (NT) {
-                    if (out) __builtin_nontemporal_store(s_eo[wid][k][lane], (__attribute__((address_space(1))) uint32_t*)(out + p));
-                    if (status) __builtin_nontemporal_store(s_es[wid][k][lane], (__attribute__((address_space(1))) uint8_t*)(status + p));
+                    if (out) __builtin_nontemporal_store(s_eo[wid][k][la], (__attribute__((address_space(1))) uint32_t*)(out + p));
+                    if (status) __builtin_nontemporal_store(s_es[wid][k][la], (__attribute__((address_space(1))) uint8_t*)(status + p));
                 } else {
-                    if (out) out[p] = s_eo[wid][k][lane];
-                    if (status) status[p] = s_es[wid][k][lane];
+                    if (out) out[p] = s_eo[wid][k][la];
+                    if (status) status[p] = s_es[wid][k][la];
                 }
             }
         }
@@ -779,14 +755,24 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
             }
         }
         bool live = P0 + lo < n;
-        uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-        if (WIN) {   // a packet that does not start in this window goes to k_win_left
-            const bool inw = off >= win.base && off - win.base < kWinBytes;
-            const uint64_t m = __ballot(live && !inw);
-            if (m != 0 && lane == 0) atomicAdd(win.left, (uint32_t)__popcll(m));
+        const uint64_t off_abs = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+        // WIN: the unit's window (its first packet's, see kWinBytes); packets starting elsewhere
+        // (pend) are done after the unit
+        uint64_t pend = 0;
+        uint64_t wb = 0;
+        if (WIN) {
+            const uint32_t wsel = __builtin_amdgcn_readfirstlane((uint32_t)(off_abs >> 31));
+            const bool inw = (uint32_t)(off_abs >> 31) == wsel;
+            pend = __ballot(live && !inw);
             live = live && inw;
-            off -= win.base;
+            wb = (uint64_t)wsel * kWinBytes;
         }
+        // the window's view of the arena (names shadowed for the pass's body)
+        const uint64_t arena_len = WIN ? (wb < arena_len_all ? min(kWinSpan, arena_len_all - wb) : 0) : arena_len_all;
+        uint8_t* const arena_w = WIN && arena_w_all ? arena_w_all + wb : arena_w_all;
+        const __amdgpu_buffer_rsrc_t rsrc =
+            WIN ? __builtin_amdgcn_make_buffer_rsrc((void*)(arena + wb), 0, (int)buf_records(arena_len), 0x00020000) : rsrc_all;
+        const uint64_t off = off_abs - wb;
         const int len = dv.z & 0xffff;
         const int l4o = dv.z >> 16;
         const int ver = dv.w & 0xff;
@@ -922,8 +908,10 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                             if (ur.do_l4) st_be16_nt(w + u_l4o2 + ur.fld, l4c);
                         }
                         if (DS && stage) {
-                            s_eo[wid][es_n][lane] = res_out;
-                            s_es[wid][es_n][lane] = (uint8_t)st;
+                            uint32_t la = (uint32_t)lane;   // opaque: see es_flush
+                            asm volatile("" : "+v"(la));
+                            s_eo[wid][es_n][la] = res_out;
+                            s_es[wid][es_n][la] = (uint8_t)st;
                         } else {
                             store_result<NT>(out, status, P0 + lo, res_out, st);
                         }
@@ -1057,8 +1045,10 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                 }
             }
             if (DS && stage) {
-                s_eo[wid][es_n][lane] = res_out;
-                s_es[wid][es_n][lane] = (uint8_t)res_st;
+                uint32_t la = (uint32_t)lane;   // opaque: see es_flush
+                asm volatile("" : "+v"(la));
+                s_eo[wid][es_n][la] = res_out;
+                s_es[wid][es_n][la] = (uint8_t)res_st;
             } else if (live) {
                 store_result<NT>(out, status, P0 + lo, res_out, res_st);
             }
@@ -1073,7 +1063,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         // ---- phase B: teams stream the packets in slot order ----
         if (TS > 0) {
             stream_tier<(TS > 0 ? TS : 1), US, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, n_small);
-            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0), WT, TRIM>(rsrc, s_slot[wid], lane, n_small, 64,
+            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0), WT>(rsrc, s_slot[wid], lane, n_small, 64,
                                              // rotated only when the tier is one cost class: in a
                                              // sorted mixed tier the wrap would pair unlike sizes
                                              (ROT && n_cls == 1) ? (blk * 4u + (uint32_t)wid) * (uint32_t)(ROT < 0 ? -ROT : ROT) : 0u);
@@ -1090,6 +1080,23 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         }
         if (!fastu) finish(sums);
         wave_sync_lds();   // slots are rewritten by the next super-iteration
+        if (WIN) {
+            // the unit's packets outside its window: one at a time, the whole wave as one team,
+            // 64-bit loads on the whole arena; results where the unit's own go (staged or stored)
+            for (uint64_t m = pend; m != 0; m &= m - 1) {
+                const int l = (int)__builtin_ctzll(m);
+                const uint4 dl = make_uint4(__builtin_amdgcn_readlane(dv.x, l), __builtin_amdgcn_readlane(dv.y, l),
+                                            __builtin_amdgcn_readlane(dv.z, l), __builtin_amdgcn_readlane(dv.w, l));
+                const int fl_l = __builtin_amdgcn_readlane(fov, l);
+                if (DS && stage)
+                    k1_packet<64, 4, VERIFY, false>(arena, arena_len_all, dl, fl_l, flags_override != nullptr, (uint32_t)l,
+                                                    &s_eo[wid][es_n][0], &s_es[wid][es_n][0], arena_w_all, lane);
+                else
+                    k1_packet<64, 4, VERIFY, NT>(arena, arena_len_all, dl, fl_l, flags_override != nullptr, P0 + (uint32_t)l,
+                                                 out, status, arena_w_all, lane);
+            }
+            wave_sync_lds();
+        }
         if (DS && stage && ++es_n == kEsUnits) {
             es_flush();
             es_P0 = Pn;
@@ -1103,98 +1110,23 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
 // count: left alone, the compiler gave them 95 and 92 (5 waves) -- the verify build for its stored
 // fields, the staging build because its 26 KB of LDS let it budget for fewer resident waves
 // (DESIGN.md §5 items 25, 28).  tests/test_kernel_resources.py holds all of them to 80, no scratch.
-template <int TEAM, int U, int TS, int US, bool VERIFY, int WPE, int IL, int ROT, bool SF, bool WT, bool DS>
+template <int TEAM, int U, int TS, int US, bool VERIFY, int WPE, int IL, int ROT, bool SF, bool WT, bool DS, bool WIN = false>
 constexpr int k2_waves_per_eu() {
     return WPE > 1 ? WPE
                    : (TEAM == kDefaultTeam && U == kDefaultUnroll && TS == kSmallTeam && US == kSmallUnroll &&
-                      IL == 0 && ROT == kDefaultRot && SF && !WT && (VERIFY || DS))
+                      IL == 0 && ROT == kDefaultRot && SF && !WT && (VERIFY || DS || WIN))
                          ? 6
                          : 1;
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool TRIM = false, bool WIN = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_per_eu<TEAM, U, TS, US, VERIFY, WPE, IL, ROT, SF, WT, DS>()))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_per_eu<TEAM, U, TS, US, VERIFY, WPE, IL, ROT, SF, WT, DS, WIN>()))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
-                                                uint8_t* __restrict__ arena_w, uint32_t low_grid, WinArg win) {
-    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS, TRIM, WIN>(arena, arena_len, desc, n, out, status, flags_override,
-                                                                       arena_w, low_grid, blockIdx.x, gridDim.x, win);
-}
-
-// Window boundaries (arenas past 4 GiB): block w in 1..nw-1 finds the first descriptor whose offset
-// is at least w x kWinBytes with a 256-way search (each round narrows the range 256-fold: 4 rounds
-// for 16M packets, a dependent load each); block 0 writes 0 and clears the leftover count, block nw
-// writes n.  Unsorted descriptors give some index: the launches take prefix maxima, so the ranges
-// still partition the batch.
-__global__ __launch_bounds__(256) void k_win_split(const uint4* __restrict__ desc, uint32_t n, uint32_t nw,
-                                                   uint32_t* __restrict__ rng, uint32_t* __restrict__ left) {
-    const uint32_t w = blockIdx.x;
-    if (w == 0 || w == nw) {
-        if (threadIdx.x == 0) {
-            rng[w] = w == 0 ? 0u : n;
-            if (w == 0) *left = 0u;
-        }
-        return;
-    }
-    const uint64_t target = (uint64_t)w * kWinBytes;
-    __shared__ uint32_t s_first;
-    uint32_t lo = 0, hi = n;   // the answer lies in [lo, hi]; hi: no descriptor of [lo, hi) qualifies
-    while (lo < hi) {
-        const uint32_t sz = hi - lo;
-        const uint32_t idx = lo + (uint32_t)(((uint64_t)sz * threadIdx.x) >> 8);
-        const uint4 d = desc[idx];
-        const bool pred = ((uint64_t)d.x | ((uint64_t)d.y << 32)) >= target;
-        if (threadIdx.x == 0) s_first = 256u;
-        __syncthreads();
-        if (pred) atomicMin(&s_first, threadIdx.x);
-        __syncthreads();
-        const uint32_t j = s_first;
-        __syncthreads();
-        if (j == 0) {
-            hi = lo;
-        } else {
-            const uint32_t prev = lo + (uint32_t)(((uint64_t)sz * (j - 1)) >> 8);
-            hi = j < 256u ? lo + (uint32_t)(((uint64_t)sz * j) >> 8) : hi;
-            lo = prev + 1;
-        }
-    }
-    if (threadIdx.x == 0) rng[w] = lo;
-}
-
-// The packets the window launches left (see kWinBytes): teams of 8 lanes walk the batch and take
-// each packet whose offset lies outside the window its index fell to, through the team kernel's
-// 64-bit path (k1_packet).  Nothing to do (address-sorted descriptors): one load, then return.
-template <bool VERIFY, bool NT>
-__global__ __launch_bounds__(256) void k_win_left(const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                  const uint4* __restrict__ desc, uint32_t n,
-                                                  uint32_t* __restrict__ out, uint8_t* __restrict__ status,
-                                                  const uint8_t* __restrict__ flags_override,
-                                                  uint8_t* __restrict__ arena_w, const uint32_t* __restrict__ rng,
-                                                  uint32_t nw, const uint32_t* __restrict__ left) {
-    if (*left == 0u) return;
-    __shared__ uint32_t s_lo[kMaxWin + 1];
-    for (uint32_t k = threadIdx.x; k <= nw; k += blockDim.x) s_lo[k] = rng[k];
-    __syncthreads();
-    if (threadIdx.x == 0)
-        for (uint32_t k = 1; k <= nw; ++k) s_lo[k] = max(s_lo[k], s_lo[k - 1]);
-    __syncthreads();
-    constexpr int TEAM = kDefaultTeam;
-    const int tl = threadIdx.x & (TEAM - 1);
-    const uint32_t nteams = gridDim.x * (256u / TEAM);
-    for (uint32_t p = (blockIdx.x * 256u + threadIdx.x) / TEAM; p < n; p += nteams) {
-        uint32_t a = 0, b = nw;   // the window of index p: the last w with s_lo[w] <= p
-        while (b - a > 1) {
-            const uint32_t m = (a + b) >> 1;
-            if (s_lo[m] <= p) a = m; else b = m;
-        }
-        const uint4 dv = desc[p];
-        const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
-        const uint64_t base = (uint64_t)a * kWinBytes;
-        if (off >= base && off - base < kWinBytes) continue;   // its window launch took it
-        k1_packet<TEAM, kDefaultUnroll, VERIFY, NT>(arena, arena_len, dv, flags_override ? flags_override[p] : 0,
-                                                    flags_override != nullptr, p, out, status, arena_w, tl);
-    }
+                                                uint8_t* __restrict__ arena_w, uint32_t low_grid) {
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS, WIN>(arena, arena_len, desc, n, out, status, flags_override,
+                                                                       arena_w, low_grid, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1413,11 +1345,11 @@ static uint32_t default_low_grid() {
     return (uint32_t)num_cus(dev) * 2u;
 }
 
-template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool TRIM = false>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, bool adapt, hipStream_t stream) {
-    if (arena_len > kMaxBufArena || ((uintptr_t)arena & 15))
+    if ((!WIN && arena_len > kMaxBufArena) || ((uintptr_t)arena & 15))
         return launch_team<TEAM, U>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w,
                                     grid > 0 ? grid : default_grid(), stream);
     uint32_t need = (n + 255) / 256;   // 4 waves x 64 packets per workgroup
@@ -1436,7 +1368,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     const uint32_t cus = (uint32_t)num_cus(dev);
 #define VPC_LAUNCH(V, N)                                                                                         \
     do {                                                                                                         \
-        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT, DS, TRIM>;                                 \
+        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT, DS, WIN>;                                  \
         uint32_t gg = g;                                                                                         \
         if (dense) {                                                                                             \
             static const uint32_t res = resident_wgs((const void*)kern);                                         \
@@ -1445,7 +1377,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
         if (gg > need) gg = need;                                                                                \
         if (gg == 0) gg = 1;                                                                                     \
         hipLaunchKernelGGL(kern, dim3(gg), dim3(256), 0, stream, arena, arena_len, (const uint4*)desc, n, out,   \
-                           status, flags_override, arena_w, low_grid, WinArg{0, nullptr, nullptr, 0});            \
+                           status, flags_override, arena_w, low_grid);                                            \
     } while (0)
     if (verify) {
         if (nt) VPC_LAUNCH(true, true); else VPC_LAUNCH(true, false);
@@ -1454,57 +1386,6 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     }
 #undef VPC_LAUNCH
     return hipGetLastError();
-}
-
-// The default K2 over an arena past 4 GiB (see kWinBytes): the window boundaries, one K2 launch per
-// window (the sampled low grid and the dense grid decided on the whole batch, as for a smaller
-// arena), and the leftover pass, all on `stream`; the boundaries live in stream-ordered scratch.
-template <bool DS>
-static hipError_t launch_dw(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
-                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
-                            uint8_t* arena_w, bool adapt, hipStream_t stream) {
-    const uint32_t nw = (uint32_t)((arena_len + kWinBytes - 1) / kWinBytes);
-    uint32_t* ctl = nullptr;
-    hipError_t e = hipMallocAsync((void**)&ctl, (size_t)(nw + 2) * sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
-    uint32_t* rng = ctl;
-    uint32_t* left = ctl + nw + 1;
-    hipLaunchKernelGGL(k_win_split, dim3(nw + 1), dim3(256), 0, stream, (const uint4*)desc, n, nw, rng, left);
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const uint32_t cus = (uint32_t)num_cus(dev);
-    const uint32_t low_grid = (!adapt || arena_len < (uint64_t)n * 1024u) ? 0u : default_low_grid();
-    const bool dense = adapt && arena_len <= (uint64_t)n * 128u;
-    const uint32_t need = (n + 255) / 256;
-#define VPC_LAUNCH_W(V, N)                                                                                        \
-    do {                                                                                                          \
-        auto kern = k_csum_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, V, N, 1, 0, kDefaultRot, true,  \
-                             false, DS, false, true>;                                                             \
-        uint32_t gg = default_grid();                                                                             \
-        if (dense) {                                                                                              \
-            static const uint32_t res = resident_wgs((const void*)kern);                                          \
-            gg = min(gg, res * cus);                                                                              \
-        }                                                                                                         \
-        gg = max(1u, min(gg, need));                                                                              \
-        for (uint32_t w = 0; w < nw; ++w) {                                                                       \
-            const uint64_t base = (uint64_t)w * kWinBytes;                                                        \
-            const uint64_t len = min(kWinSpan, arena_len - base);                                                 \
-            hipLaunchKernelGGL(kern, dim3(gg), dim3(256), 0, stream, arena + base, len, (const uint4*)desc, n, out, \
-                               status, flags_override, arena_w ? arena_w + base : nullptr, low_grid,               \
-                               WinArg{base, rng, left, w});                                                       \
-        }                                                                                                         \
-        hipLaunchKernelGGL((k_win_left<V, N>), dim3(cus * 8u), dim3(256), 0, stream, arena, arena_len,            \
-                           (const uint4*)desc, n, out, status, flags_override, arena_w, rng, nw, left);           \
-    } while (0)
-    if (verify) {
-        if (nt) VPC_LAUNCH_W(true, true); else VPC_LAUNCH_W(true, false);
-    } else {
-        if (nt) VPC_LAUNCH_W(false, true); else VPC_LAUNCH_W(false, false);
-    }
-#undef VPC_LAUNCH_W
-    e = hipGetLastError();
-    const hipError_t ef = hipFreeAsync(ctl, stream);
-    return e != hipSuccess ? e : ef;
 }
 
 hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
@@ -1554,20 +1435,16 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 76: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         // 78: the team kernel with 64-bit loads, which serves arenas past 4 GiB (A/B, tooling)
         case 78: return launch_team<kDefaultTeam, kDefaultUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid > 0 ? grid : (int)default_grid(), stream);
-        // 80 / 81: the default's staged / unstaged build with trimmed trips (TRIM, A/B)
-        case 80: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
-        case 81: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         // 79: the staging build on every batch (round 3's r03w default, A/B)
         case 79: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 70:
         case 0:
-            // Arenas past 4 GiB: K2 per 2-GiB window (see kWinBytes) -- larger than any window
-            // table, or not 16-B aligned: the team kernel (launch_d's fallback)
-            if (grid <= 0 && arena_len > kMaxBufArena && !((uintptr_t)arena & 15) &&
-                arena_len <= (uint64_t)kMaxWin * kWinBytes) {
-                if (adapt && arena_len <= (uint64_t)n * 128u)
-                    return launch_dw<false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, adapt, stream);
-                return launch_dw<true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, adapt, stream);
+            // Arenas past 4 GiB: K2 with a pass per 2-GiB window its units' packets start in (see
+            // kWinBytes); not 16-B aligned: the team kernel (launch_d's fallback)
+            if (arena_len > kMaxBufArena) {
+                if (grid <= 0 && adapt && arena_len <= (uint64_t)n * 128u)
+                    return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+                return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
             }
             // Dense small frames (at most 128 arena bytes per packet: C1) never stage their result
             // words: they take the build without staging and its smaller LDS
