@@ -112,7 +112,7 @@ def resummarise(tag):
 def main(tag):
     os.makedirs(P, exist_ok=True)
     prov = provenance(tag)
-    for cfg in ("c2", "c1", "c3", "c4", "c4_strong", "c5"):
+    for cfg in ("c2", "c1", "c3", "c4", "c4_strong", "c5", "c4s_8rank", "c5_8rank", "c2_2rank", "c5_2rank"):
         d = json_line(os.path.join(G, f"{tag}_bench_{cfg}.log"))
         if d:
             json.dump(d, open(os.path.join(P, f"{tag}_bench_{cfg}.json"), "w"), indent=1)
@@ -129,6 +129,12 @@ def main(tag):
     d = json_line(os.path.join(G, f"{tag}_hostpath.log"))
     if d:
         json.dump(d, open(os.path.join(P, f"{tag}_hostpath_c2.json"), "w"), indent=1)
+    fl = os.path.join(G, f"{tag}_flush.log")   # tools/flush_latency: one JSON object per line
+    if os.path.exists(fl):
+        rows = [json.loads(x) for x in open(fl) if x.startswith("{")]
+        if rows:
+            json.dump({"src_hash": prov["src_hash"], "head": prov["head"], "rows": rows},
+                      open(os.path.join(P, f"{tag}_flush_latency.json"), "w"), indent=1)
     print("saved", sorted(f for f in os.listdir(P) if f.startswith(tag)))
 
 

@@ -392,6 +392,13 @@ __device__ __forceinline__ void wave_sync_lds() {
 // of a 64-bit add's two, and one accumulator register instead of two.
 __device__ __forceinline__ uint32_t hsum(uint32_t acc, uint32_t w) { return __builtin_amdgcn_sad_u16(w, 0u, acc); }
 
+// Halfword h (0..7) of a 16-B chunk held as four dwords, little-endian.
+__device__ __forceinline__ uint32_t pick_half(const uint32_t (&w)[4], uint32_t h) {
+    const uint32_t lo = (h & 2u) ? w[1] : w[0], hi = (h & 2u) ? w[3] : w[2];
+    const uint32_t d = (h & 4u) ? hi : lo;
+    return (h & 1u) ? d >> 16 : d & 0xffffu;
+}
+
 // Fast-class trips of one team over its packet's chunks [0, nch): U loads per lane issued
 // back to back, then consumed (payload fast path, masked tail, header bitmaps).  Verify: the
 // stored checksum fields are one halfword each (the fast class has L3 and L4 at even offsets),
@@ -432,14 +439,12 @@ __device__ __forceinline__ void fast_trips(const __amdgpu_buffer_rsrc_t rsrc, ui
                     acc_l4 = hsum(acc_l4, w[j] & hmask((bm.y >> hb) & 3));
                 }
                 if (VERIFY) {
-                    uint32_t sz = 0, sw = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        sz += w[j] & hmask((bm.z >> (hb0 + 2 * j)) & 3);
-                        sw += w[j] & hmask((bm.w >> (hb0 + 2 * j)) & 3);
-                    }
-                    if ((bm.z >> hb0) & 0xffu) st_slot[1] = (uint16_t)fold32(sz);
-                    if ((bm.w >> hb0) & 0xffu) st_slot[0] = (uint16_t)fold32(sw);
+                    // each field bitmap holds one bit, the field's halfword in the first 64 B
+                    // (chunk = bit >> 3): the lane of that chunk picks the halfword directly
+                    const uint32_t fz = (uint32_t)__builtin_ctz(bm.z | 0x80000000u);
+                    const uint32_t fw = (uint32_t)__builtin_ctz(bm.w | 0x80000000u);
+                    if (bm.z && (int)(fz >> 3) == k) st_slot[1] = (uint16_t)pick_half(w, fz & 7u);
+                    if (bm.w && (int)(fw >> 3) == k) st_slot[0] = (uint16_t)pick_half(w, fw & 7u);
                 }
             }
             asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
