@@ -844,6 +844,62 @@ def test_staged_result_stores(V, orc):
     assert np.array_equal(arena.cpu().numpy(), a)
 
 
+@pytest.mark.parametrize("team", [0, 84])
+def test_workgroup_sorted_units(V, orc, team):
+    """Mixed batches large enough for the sampled grid, where the 4 waves of a workgroup rank
+    their 256 packets by cost class together (the default, and variant 84):
+    C3 packets with bad descriptors, raw ranges, runs of small packets of one shape (window-unit
+    candidates, which workgroup-sorted units do not take), n not a multiple of 256 (waves past the
+    batch in the last workgroup) and more units than one grid-stride round.  Verify, compute and
+    write modes equal the oracle's, and variant 76 (per-wave units) equals both."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = cus * 12 * 256 + 100_000 + 37            # a second grid-stride round for some workgroups
+    a, d = orc.synth(n, 2048, 0, O.SYNTH_C3, O.SEED, 84)
+    sampled = {(n * lane) >> 6 for lane in range(64)}
+    rng = np.random.default_rng(84)
+    pick = np.array(sorted(set(rng.choice(n, 6000, replace=False).tolist()) - sampled))
+    d = d.copy()
+    d["l3_len"][pick[:500]] = 0                    # bad: shorter than an IPv4 header
+    d["l3_off"][pick[500:800]] = a.size + 4096     # bad: outside the arena
+    d["flags"][pick[800:900]] = O.F_RAW            # raw ranges
+    # units of 64 packets of one small shape (window units in per-wave mode): C3's own 64-B
+    # IPv4/UDP packets copied over whole units
+    small = np.flatnonzero((d["l3_len"] == 64) & (d["l3_ver"] == 4) & (d["l4_proto"] == 17))
+    src = int(small[0])
+    for u in (1000, 1001, 2500):
+        for i in range(u * 64, u * 64 + 64):
+            a[i * 2048:(i + 1) * 2048] = a[src * 2048:(src + 1) * 2048]
+            d[i] = d[src]
+            d["l3_off"][i] = d["l3_off"][src] - src * 2048 + i * 2048
+    want, want_st = orc.process(a, d, O.MODE_VERIFY, threads=8)
+    arena = dev(a)
+    dt = V.desc_to_tensor(d)
+    for v in (team, 76):
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        st = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        V.compute(arena, dt, n, out, st, O.MODE_VERIFY, v)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want), v
+        assert np.array_equal(st.cpu().numpy(), want_st), v
+        out.zero_()
+        V.compute(arena, dt, n, out, None, O.MODE_COMPUTE, v)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want), v
+    w_out, _ = orc.process(a, d, O.MODE_COMPUTE, write=True)   # a now holds the written frames
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    V.compute(arena, dt, n, out, None, O.MODE_WRITE, team)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), w_out)
+    assert np.array_equal(arena.cpu().numpy(), a)
+    # the frames now hold their sums: verify reports every requested one as correct
+    V.compute(arena, dt, n, None, st, O.MODE_VERIFY, team)
+    torch.cuda.synchronize()
+    ok = np.where(d["flags"] & O.F_IP, O.S_IP_OK, 0) | np.where(d["flags"] & O.F_L4, O.S_L4_OK, 0)
+    sel = ((want_st & O.S_DONE) != 0) & ((d["flags"] & O.F_RAW) == 0)
+    assert np.array_equal(st.cpu().numpy()[sel] & (O.S_IP_OK | O.S_L4_OK), ok.astype(np.uint8)[sel])
+
+
 # ---- low-latency service (persistent grid polling a pinned mailbox) ----
 
 def _busy_us(us):

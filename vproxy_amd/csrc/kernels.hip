@@ -378,6 +378,14 @@ static hipError_t launch_team(const uint8_t* arena, uint64_t arena_len, const vp
 // and the sort puts packets of similar length in the same iteration, so a ragged batch
 // (C3) no longer pays the longest of PPI random packets per iteration.
 // ------------------------------------------------------------------------------------------
+// Workgroup barrier for LDS exchange between waves: waits for LDS operations only (the fences
+// name the local address space), not for the wave's outstanding global loads and stores.
+__device__ __forceinline__ void wg_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
     // LDS instructions of one wave execute in program order, so lanes exchanging data through
     // LDS only need the compiler not to move accesses across this point (no memory fence: a
@@ -513,9 +521,11 @@ __device__ __forceinline__ void tier_team(const __amdgpu_buffer_rsrc_t rsrc, uin
 // packets per iteration.  WT: a last iteration that fills at most half of its teams (the tail of
 // the tier's costliest class, in a size-sorted unit) runs with teams of 2 x TEAM lanes, so its
 // packets need half the trips.
+// it0 / istep: the iterations this wave takes (workgroup-sorted units: every fourth, from the
+// wave index).
 template <int TEAM, int U, bool VERIFY, bool NT, bool SLOTROT = false, bool WT = false>
 __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, uint4 (*slots)[4], int lane,
-                                            int s_begin, int s_end, uint32_t rot = 0) {
+                                            int s_begin, int s_end, uint32_t rot = 0, int it0 = 0, int istep = 1) {
     constexpr int PPI = 64 / TEAM;
     const int tl = lane & (TEAM - 1);
     const int tid = lane / TEAM;
@@ -528,7 +538,7 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
     const bool wide = WT && TEAM <= 16 && rot == 0 && rem > 0 && 2 * rem <= PPI;
     if (wide) --nit;
 #pragma unroll 1
-    for (int it = 0; it < nit; ++it) {
+    for (int it = it0; it < nit; it += istep) {
         int sidx;
         bool act;
         if (SLOTROT) {   // rotation by slots: the wave's first packet is slot r0
@@ -541,7 +551,7 @@ __device__ __forceinline__ void stream_tier(const __amdgpu_buffer_rsrc_t rsrc, u
         }
         tier_team<TEAM, U, VERIFY, NT>(rsrc, slots, tl, sidx, act);
     }
-    if (WT && TEAM <= 16 && wide) {
+    if (WT && TEAM <= 16 && wide && it0 == 0) {
         constexpr int T2 = TEAM <= 16 ? 2 * TEAM : TEAM;
         const int sidx = s_begin + nit * PPI + lane / T2;
         tier_team<T2, U, VERIFY, NT>(rsrc, slots, lane & (T2 - 1), sidx, sidx < s_end);
@@ -665,7 +675,8 @@ constexpr uint64_t kWinSpan = kWinBytes + 65536;
 // k_csum_service: the persistent service grid, once per batch).
 // ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
 // ROT > 0 rotates whole iterations (64 / TEAM packets), ROT < 0 single slots.
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false>
+// WGS: workgroup-sorted units on mixed batches (below).
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false, bool WGS = false>
 __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -704,10 +715,19 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         dnext = desc[P0 + lo];
         if (flags_override) fnext = flags_override[P0 + lo];
     }
+    // Workgroup-sorted units (WGS, wg): on a batch the sample found mixed (some packets < 1 KiB,
+    // some > 64 B: C3), the 4 waves of a workgroup rank their 256 packets by cost class together
+    // and stream the workgroup's slots in one order, each wave every fourth iteration of a tier.
+    // A wave's own 64 packets hold a class of C3 in a few iterations, the last one partly empty;
+    // across 256 such tails are rarer.  Three workgroup barriers per unit (class counts, slots,
+    // sums), no window units (the sample rules out all-small batches, where they apply), and the
+    // 4 waves run the same number of units.  DESIGN.md §5 item 31.
+    bool wg = false;
     if (sample) {
         const uint4 sd = desc[(uint32_t)(((uint64_t)n * (uint32_t)lane) >> 6)];
         if (__ballot((sd.z & 0xffffu) >= 1024u) == ~0ull) grid = low_grid;
         if (blk >= grid) return;   // whole workgroup, before any LDS use
+        if (WGS && !WIN && grid == gdim && n < 0xffff0000u) wg = __ballot((sd.z & 0xffffu) > 64u) != 0ull;
         if (!early && P0 + lo < n) {
             dnext = desc[P0 + lo];
             if (flags_override) fnext = flags_override[P0 + lo];
@@ -747,7 +767,15 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         }
         es_n = 0;
     };
-    for (uint32_t Pn; P0 < n; P0 = Pn) {
+    uint4 (*const flat)[4] = &s_slot[0][0];   // the workgroup's 256 slots (wave w's at 64 w)
+    __shared__ uint32_t s_wcnt[16];           // wg: byte w of word b = packets of class b in wave w's unit
+    // wg: the loop runs while the workgroup's first packet is in the batch (all 4 waves alike)
+    // The unit loop, instantiated twice in the WGS build: with workgroup-sorted units (WGM) and
+    // without, so that the batches the sample does not find mixed run the per-wave code as it is
+    // in the builds without WGS (one loop with a runtime mode cost C2 0.9%)
+    auto unit_loop = [&](auto wgm_tag) {
+    constexpr bool WGM = decltype(wgm_tag)::value;
+    for (uint32_t Pn; (WGM ? P0 - (uint32_t)wid * 64u : P0) < n; P0 = Pn) {
         // ---- phase A: this lane's packet ----
         const uint4 dv = dnext;
         const int fov = fnext;
@@ -800,7 +828,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         // per instruction) into its LDS slots, and every lane sums its own packet from L3-aligned
         // dwords, where the header fields sit at fixed dwords: no plan, no sort, no team
         // reduction, no per-dword masks.  The sums have K2's slot format.
-        if (SF) {
+        if (SF && !WGM) {
             const uint32_t boff = (uint32_t)off & ~15u;
             const uint32_t base = __builtin_amdgcn_readfirstlane(boff);
             const uint32_t rel = boff - base;
@@ -986,17 +1014,39 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                 else key = fastc ? 2 + min((pl.nch + TEAM * U - 1) / (TEAM * U), 12) : 15;
             }
             uint32_t rank = 0, cnt = 0;
+            uint32_t kc = 0, kp = 0;   // wg: lane b holds class b's count and offset in this wave
             for (int b = 0; b < 16 && cnt < 64; ++b) {
                 const uint64_t m = __ballot(key == b);
                 if (key == b)
                     rank = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (WGS && lane == b) {
+                    kc = (uint32_t)__popcll(m);
+                    kp = cnt;
+                }
                 cnt += (uint32_t)__popcll(m);
                 if (b >= 2 && m) ++n_cls;
                 if (b == 1) n_small = (int)cnt;   // keys 0 and 1 go to the small tier
             }
-            key = (int)rank;   // from here on: this packet's slot
+            uint32_t si = (uint32_t)wid * 64u + rank;   // this packet's slot among the workgroup's 256
+            if (WGM) {
+                // class b's slots: after all classes < b of the workgroup, then those of waves < wid
+                if (lane < 16) ((uint8_t*)&s_wcnt[lane])[wid] = (uint8_t)kc;
+                wg_sync_lds();
+                const uint32_t cw = lane < 16 ? s_wcnt[lane] : 0u;   // the 4 waves' counts of class `lane`
+                const uint32_t tot = __builtin_amdgcn_sad_u8(cw, 0u, 0u);
+                const uint32_t before = __builtin_amdgcn_sad_u8(cw & ((1u << (8 * wid)) - 1u), 0u, 0u);
+                uint32_t incl = tot;   // prefix over lanes 0..15 (one DPP row)
+                incl = dpp_add<0x111>(incl);
+                incl = dpp_add<0x112>(incl);
+                incl = dpp_add<0x114>(incl);
+                incl = dpp_add<0x118>(incl);
+                const uint32_t first = incl - tot + before - kp;   // class b's first slot, minus its offset here
+                si = (uint32_t)__builtin_amdgcn_ds_bpermute(key << 2, (int)first) + rank;
+                n_small = __builtin_amdgcn_readlane((int)(incl - tot), 2);
+            }
+            key = (int)si;   // from here on: this packet's slot
             {
-                uint4* sl = s_slot[wid][rank];
+                uint4* sl = flat[si];
                 sl[0] = make_uint4(boff, (uint32_t)pl.nch | ((uint32_t)klo << 16) | ((uint32_t)do_ip << 30) | ((uint32_t)fastc << 31),
                                    kfast, (uint32_t)pl.l4hi);
                 sl[1] = make_uint4(B_ip, B_l4, F_ip, F_l4);
@@ -1063,25 +1113,34 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         if (fastu) {
             sums = fsums;   // finished above
         } else {
-        wave_sync_lds();
-
         // ---- phase B: teams stream the packets in slot order ----
+        if (WGM) wg_sync_lds();
+        else wave_sync_lds();
+        // WGM: the workgroup's 256 slots, each wave taking every fourth iteration of a tier, the
+        // large tier's round continuing after the wave that took the small tier's last one (the
+        // wave's own 64 slots otherwise)
+        uint4 (*const tslots)[4] = WGM ? flat : s_slot[wid];
+        const int t_end = WGM ? 256 : 64;
+        const int it0 = WGM ? wid : 0, istep = WGM ? 4 : 1;
         if (TS > 0) {
-            stream_tier<(TS > 0 ? TS : 1), US, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, n_small);
-            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0), WT>(rsrc, s_slot[wid], lane, n_small, 64,
+            stream_tier<(TS > 0 ? TS : 1), US, VERIFY, NT>(rsrc, tslots, lane, 0, n_small, 0u, it0, istep);
+            const int it0l = WGM ? (it0 + 4 - (((n_small + 64 / (TS > 0 ? TS : 1) - 1) / (64 / (TS > 0 ? TS : 1))) & 3)) & 3 : 0;
+            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0), WT>(rsrc, tslots, lane, n_small, t_end,
                                              // rotated only when the tier is one cost class: in a
                                              // sorted mixed tier the wrap would pair unlike sizes
-                                             (ROT && n_cls == 1) ? (blk * 4u + (uint32_t)wid) * (uint32_t)(ROT < 0 ? -ROT : ROT) : 0u);
+                                             (ROT && n_cls == 1 && !WGM) ? (blk * 4u + (uint32_t)wid) * (uint32_t)(ROT < 0 ? -ROT : ROT) : 0u,
+                                             it0l, istep);
         } else {
-            stream_tier<TEAM, U, VERIFY, NT>(rsrc, s_slot[wid], lane, 0, 64);
+            stream_tier<TEAM, U, VERIFY, NT>(rsrc, tslots, lane, 0, t_end, 0u, it0, istep);
         }
-        wave_sync_lds();
+        if (WGM) wg_sync_lds();
+        else wave_sync_lds();
         // The next unit's descriptor (loaded a whole unit ago) is taken into registers here,
         // before this unit's stores: vmcnt counts loads and stores together, so a wait for it
         // after the stores would stall the wave until they complete, once per unit.
         asm volatile("" ::"v"(dnext.x), "v"(dnext.y), "v"(dnext.z), "v"(dnext.w), "v"(fnext));
-        sums = s_slot[wid][key][0];
-        if (VERIFY) sums.w = s_slot[wid][key][3].w;   // stored fields {l4, ip << 16}
+        sums = flat[key][0];
+        if (VERIFY) sums.w = flat[key][3].w;   // stored fields {l4, ip << 16}
         }
         if (!fastu) finish(sums);
         wave_sync_lds();   // slots are rewritten by the next super-iteration
@@ -1107,6 +1166,9 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
             es_P0 = Pn;
         }
     }
+    };
+    if (WGS && wg) unit_loop(std::integral_constant<bool, WGS>{});
+    else unit_loop(std::false_type{});
     if (DS && stage) es_flush();
 }
 
@@ -1115,22 +1177,22 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
 // count: left alone, the compiler gave them 95 and 92 (5 waves) -- the verify build for its stored
 // fields, the staging build because its 26 KB of LDS let it budget for fewer resident waves
 // (DESIGN.md §5 items 25, 28).  tests/test_kernel_resources.py holds all of them to 80, no scratch.
-template <int TEAM, int U, int TS, int US, bool VERIFY, int WPE, int IL, int ROT, bool SF, bool WT, bool DS, bool WIN = false>
+template <int TEAM, int U, int TS, int US, bool VERIFY, int WPE, int IL, int ROT, bool SF, bool WT, bool DS, bool WIN = false, bool WGS = false>
 constexpr int k2_waves_per_eu() {
     return WPE > 1 ? WPE
                    : (TEAM == kDefaultTeam && U == kDefaultUnroll && TS == kSmallTeam && US == kSmallUnroll &&
-                      IL == 0 && ROT == kDefaultRot && SF && !WT && (VERIFY || DS || WIN))
+                      IL == 0 && ROT == kDefaultRot && SF && !WT && (VERIFY || DS || WIN || WGS))
                          ? 6
                          : 1;
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_per_eu<TEAM, U, TS, US, VERIFY, WPE, IL, ROT, SF, WT, DS, WIN>()))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false, bool WGS = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_per_eu<TEAM, U, TS, US, VERIFY, WPE, IL, ROT, SF, WT, DS, WIN, WGS>()))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
                                                 uint8_t* __restrict__ arena_w, uint32_t low_grid) {
-    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS, WIN>(arena, arena_len, desc, n, out, status, flags_override,
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS, WIN, WGS>(arena, arena_len, desc, n, out, status, flags_override,
                                                                        arena_w, low_grid, blockIdx.x, gridDim.x);
 }
 
@@ -1350,7 +1412,7 @@ static uint32_t default_low_grid() {
     return (uint32_t)num_cus(dev) * 2u;
 }
 
-template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false, bool WGS = false>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, bool adapt, hipStream_t stream) {
@@ -1373,7 +1435,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     const uint32_t cus = (uint32_t)num_cus(dev);
 #define VPC_LAUNCH(V, N)                                                                                         \
     do {                                                                                                         \
-        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT, DS, WIN>;                                  \
+        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT, DS, WIN, WGS>;                             \
         uint32_t gg = g;                                                                                         \
         if (dense) {                                                                                             \
             static const uint32_t res = resident_wgs((const void*)kern);                                         \
@@ -1442,6 +1504,11 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 78: return launch_team<kDefaultTeam, kDefaultUnroll>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid > 0 ? grid : (int)default_grid(), stream);
         // 79: the staging build on every batch (round 3's r03w default, A/B)
         case 79: return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+        // 84: the default for non-dense batches (the staging build with workgroup-sorted units on
+        // mixed batches); 79 is the same build without the workgroup sort
+        case 84:
+            if (arena_len > kMaxBufArena) return hipErrorInvalidValue;
+            return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 70:
         case 0:
             // Arenas past 4 GiB: K2 with a pass per 2-GiB window its units' packets start in (see
@@ -1455,7 +1522,9 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
             // words: they take the build without staging and its smaller LDS
             if (grid <= 0 && adapt && arena_len <= (uint64_t)n * 128u)
                 return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, false>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
-            return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
+            // everything else: the staging build, whose mixed batches take workgroup-sorted units
+            // (k2_run WGS)
+            return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         default: return hipErrorInvalidValue;   // unknown kernel variant id
     }
 #undef VPC_T
