@@ -844,6 +844,32 @@ def test_staged_result_stores(V, orc):
     assert np.array_equal(arena.cpu().numpy(), a)
 
 
+@pytest.mark.parametrize("cfg", ["c1", "c3"])
+def test_status_bytes_at_any_alignment(V, orc, cfg):
+    """Status bytes of whole units go out as one dword per 4 packets when the unit's bytes start
+    4-B aligned, as bytes otherwise (K2 store_result PACK): a status buffer at offsets 0..3 of a
+    larger one, window units (C1 dense frames) and the team path (C3), a partial last unit.  Every
+    byte equals the oracle's and nothing outside [off, off + n) is written."""
+    import torch
+    sid, stride = {"c1": (O.SYNTH_C1, 64), "c3": (O.SYNTH_C3, 2048)}[cfg]
+    n = 20_000 + 37
+    a, d = orc.synth(n, stride, 0, sid, O.SEED, 7)
+    d = d.copy()
+    d["l3_len"][100:164:3] = 0                     # bad descriptors inside a few units
+    want, want_st = orc.process(a, d, O.MODE_VERIFY, threads=8)
+    arena = dev(a)
+    dt = V.desc_to_tensor(d)
+    for off in range(4):
+        buf = torch.full((n + 8,), 0xEE, dtype=torch.uint8, device="cuda")
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        V.compute(arena, dt, n, out, buf[off:off + n], O.MODE_VERIFY)
+        torch.cuda.synchronize()
+        b = buf.cpu().numpy()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want), off
+        assert np.array_equal(b[off:off + n], want_st), off
+        assert (b[:off] == 0xEE).all() and (b[off + n:] == 0xEE).all(), off
+
+
 @pytest.mark.parametrize("team", [0, 84])
 def test_workgroup_sorted_units(V, orc, team):
     """Mixed batches large enough for the sampled grid, where the 4 waves of a workgroup rank
