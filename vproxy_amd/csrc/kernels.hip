@@ -594,8 +594,8 @@ __device__ __forceinline__ DescRules desc_rules(int len, int l4o, int ver, int p
     return r;
 }
 
-// Sums of a window unit's packet in K2's slot format {l4, ip, 0, stored l4 | stored ip << 16}
-// from x = the packet's chunks (20 dwords from its chunk-aligned start).  L3 starts at dword Q
+// Sums of a window unit's packet in K2's slot format {l4, ip, 0, stored ip << 16} (the caller adds
+// the stored L4 field, read from LDS) from x = the packet's chunks (20 dwords from its chunk-aligned start).  L3 starts at dword Q
 // + sh bytes (sh 0 or 2: even offsets only), so a[k] = alignbyte(x[Q+k+1], x[Q+k], sh) is L3
 // dword k, little-endian, and with IPv4 of 20 B or IPv6 of 40 B every field is at a fixed
 // dword: IP checksum a[2] high half, pseudo addresses a[3..4] / a[2..9], the L4 checksum at
@@ -613,7 +613,7 @@ __device__ __forceinline__ uint4 win_sums(const uint32_t (&x)[20], int sh, int v
     const int nd = (len + 3) >> 2;
     const uint32_t tail = (len & 3) ? (0xffffffffu >> (8 * (4 - (len & 3)))) : 0xffffffffu;
     uint32_t ip = 0, l4 = 0;   // halfword sums (hsum)
-    uint32_t st_ip = 0, st_l4 = 0;
+    uint32_t st_ip = 0;
     if (do_ip) {   // IPv4 only (checked with the descriptor)
         ip = hsum(hsum(hsum(hsum(hsum(0u, a[0]), a[1]), a[2] & 0xffffu), a[3]), a[4]);
         st_ip = a[2] >> 16;
@@ -634,15 +634,12 @@ __device__ __forceinline__ uint4 win_sums(const uint32_t (&x)[20], int sh, int v
             if (k >= l4d && k < nd) {
                 uint32_t w = a[k];
                 if (k == nd - 1) w &= tail;
-                if (k == fd) {
-                    st_l4 = (fo & 2) ? w >> 16 : w & 0xffffu;
-                    w &= fkeep;
-                }
+                if (k == fd) w &= fkeep;   // the stored field itself: read from LDS by the caller
                 if (!psonly) l4 = hsum(l4, w);
             }
         }
     }
-    return make_uint4(fold32(l4), fold32(ip), 0u, VERIFY ? (st_l4 | (st_ip << 16)) : 0u);
+    return make_uint4(fold32(l4), fold32(ip), 0u, VERIFY ? (st_ip << 16) : 0u);
 }
 
 // One packet's result word and status byte, stored where the unit's owner lanes store them.  The
@@ -901,11 +898,19 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                         x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
                     }
                     const int u_fl = (int)((u_kd >> 16) & 0xff), u_proto = (int)((u_kd >> 8) & 0xff);
+                    // verify: the stored L4 field, one LDS halfword at a wave-uniform offset from the
+                    // lane's window (instead of a select per dword of win_sums' unrolled loop)
+                    uint32_t st_l4f = 0;
+                    if (VERIFY && ur.do_l4) {
+                        const uint32_t fb = (uint32_t)u_r0 + (u_ver == 4 ? 20u : 40u) + (uint32_t)ur.fld;
+                        st_l4f = *(const uint16_t*)((const uint8_t*)&win[win_slot(c0 + (fb >> 4))] + (fb & 15u));
+                    }
                     const int q = u_r0 >> 2;
                     if (q == 0) fsums = win_sums<0, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
                     else if (q == 1) fsums = win_sums<1, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
                     else if (q == 2) fsums = win_sums<2, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
                     else fsums = win_sums<3, VERIFY>(x, u_r0 & 3, u_ver, u_proto, u_len, u_fl);
+                    if (VERIFY) fsums.w |= st_l4f;
                     // phase C of a window unit, on the unit's (scalar) descriptor values: the
                     // same arithmetic as finish() below, without its per-lane branches
                     {
