@@ -242,3 +242,27 @@ def test_egress_descriptor_short_frames_and_ext_chains():
     d = S.egress_descriptor(v6, 0, 2)
     assert int(d["l4_proto"]) == 60 and int(d["l4_off"]) == 48
     assert S.egress_descriptor(v6[:54], 0, 2) is None      # the extension header cut off
+
+
+@pytest.mark.gpu
+def test_egress_frames_large_mixed_batch(V, orc):
+    """A flush large and mixed enough for the checksum kernel's sampled grid and its workgroup-sorted
+    units, reached through vpcsum_ctx_egress_frames: 150,000 C3 frames in
+    2-KB umem frames, registered (zero-copy), per-frame flags from the parse (the kernel's flags
+    override), every third frame asking for the L4 sum only.  The umem equals the oracle's full
+    recompute."""
+    from vproxy_amd import vswitch as S
+    n, stride = 150_000, 2048
+    arena, d = orc.synth(n, stride, 14, O.SYNTH_C3, O.SEED, 31)
+    frames = arena.reshape(n, stride)
+    frames[:, 12], frames[:, 13] = 0x08, 0x00          # Ethernet type IPv4 before each L3 packet
+    d = d.copy()
+    d["flags"][::3] = O.F_L4
+    want = arena.copy()
+    orc.process(want, d, O.MODE_COMPUTE, write=True, threads=8)
+    b = S.FrameEgressBatch(arena, capacity=n)
+    for i in range(n):
+        assert b.defer(i * stride, 14 + int(d["l3_len"][i]), int(d["flags"][i]))
+    assert b.complete_tx() == n and not b.handed_back
+    assert np.array_equal(arena, want)
+    b.close()
