@@ -25,8 +25,12 @@ Correctness gate: rank 0's GPU results are compared word for word with the oracl
 the cpu_baseline leg processes (the whole batch when its budget allows); every rank also writes its
 sums in place and verifies them (size-independent property).
 
+`--workload c5 --preimage`: C5's frames after Java's setters (new addresses and ports, stale sums)
+with the 16-B pre-images of the old values; a step is the egress flush that updates their sums
+from the pre-images (vpcsum_pre_async, RFC 1624, only the headers read).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c1|c3|c4|c5] [--strong]
-       [--share-gpu]   (more ranks than GPUs: a same-card rehearsal, reported as such)
+       [--preimage] [--share-gpu]   (more ranks than GPUs: a same-card rehearsal, reported as such)
 """
 from __future__ import annotations
 
@@ -47,6 +51,9 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level pa
 METRIC = "device-resident GB/s, batched IPv4+TCP checksum, 1500B pkts, 1/2/4/8 GPU"
 SEED = 0x20241020
 NAT_BYTES_PER_PKT = 72   # 40 B header read + 16 B rewrite + 12 B rewritten + 4 B sums
+# c5 --preimage (the egress flush of NAT'd frames, VPCSUM_F_PRE): 16 B descriptor + 16 B pre-image
+# read + 40 B header read + 4 B sums written
+PRE_BYTES_PER_PKT = 76
 # The timed launches rotate over batches whose arenas hold at least this many bytes together, so
 # that no launch reads input the 256-MB Infinity Cache kept from the previous one (C1's whole
 # 64-MB batch would otherwise be served from it: +10%)
@@ -239,6 +246,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--strong", action="store_true", help="split one global batch over the GPUs (c5: always)")
+    ap.add_argument("--preimage", action="store_true",
+                    help="c5: time the egress flush of the NAT'd frames from their pre-images (VPCSUM_F_PRE) "
+                         "instead of the NAT rewrite")
     ap.add_argument("--team", type=int, default=0, help="kernel variant id (0 = library default)")
     ap.add_argument("--ramp-ms", type=float, default=3000.0,
                     help="run the step kernel this long before the warm-up (clock ramp; reported)")
@@ -272,6 +282,12 @@ def main():
 
     synth_id, n_cfg, stride, desc_text = WORKLOADS[args.workload]
     nat = args.workload == "c5"
+    pre = nat and args.preimage
+    if args.preimage and not nat:
+        sys.exit("bench.py: --preimage is a c5 workload option")
+    if pre:
+        desc_text = ("C5 egress flush of NAT'd frames from 16-B pre-images (RFC 1624, VPCSUM_F_PRE) of "
+                     "10,000,000 x L3 1500 B IPv4 TCP/UDP after Java's setters (src/dst IP + ports)")
     strong = args.strong or nat
     stream = torch.cuda.current_stream()
     if strong:
@@ -310,10 +326,34 @@ def main():
         rw_np["mask"] = V.NAT_SRC | V.NAT_DST | V.NAT_SPORT | V.NAT_DPORT
         rw_np = np.ascontiguousarray(rw_np[first:first + n])
         rw = torch.from_numpy(rw_np.view(np.uint8).copy()).cuda()
-        bytes_per_step = n * NAT_BYTES_PER_PKT
+        bytes_per_step = n * (PRE_BYTES_PER_PKT if pre else NAT_BYTES_PER_PKT)
+        pre_img = None
+
+        def prep_pre():
+            # the frames as the egress flush receives them: the pre-image of the old addresses and
+            # ports (16-B vpcsum_pre4_t), then Java's setters (new bytes, stale sums; plumbing,
+            # emulating Ipv4Packet.setSrc / setDst and Tcp/UdpPacket.setSrcPort / setDstPort),
+            # then F_PRE on every descriptor.  Synthetic C5: L3 at the frame start, IHL 5.
+            fr = arena.view(n, stride)
+            p4 = torch.zeros((n, 16), dtype=torch.uint8, device="cuda")
+            p4[:, 0:8] = fr[:, 12:20]
+            p4[:, 8:12] = fr[:, 20:24]
+            p4[:, 12] = V.NAT_SRC | V.NAT_DST | V.NAT_SPORT | V.NAT_DPORT
+            rw2 = rw.view(n, 16)
+            fr[:, 12:20] = rw2[:, 0:8]
+            fr[:, 20:24] = rw2[:, 8:12]
+            d.view(n, 16)[:, 14] |= V.F_PRE
+            torch.cuda.synchronize()
+            return p4
+
+        if pre and n:
+            pre_img = prep_pre()
 
         def step(i=0):
-            V.nat4(arena, d, rw, n, None, V.NAT_RFC1624, stream=stream)
+            if pre:
+                V.pre(arena, d, pre_img, n, None, None, V.MODE_WRITE, V.PRE_FMT_PRE4, stream=stream)
+            else:
+                V.nat4(arena, d, rw, n, None, V.NAT_RFC1624, stream=stream)
     else:
         bytes_per_step = algorithmic_bytes(desc_np)
         ds = d_alls
@@ -459,12 +499,19 @@ def main():
     elif nat and n:
         # NAT's own memory operations with no rewrite (vpcsum_nat4_pattern_probe_async: descriptor
         # and entry reads, the header window loads, the one store of [L3+10, checksum end)),
-        # priced in the same 72 algorithmic B/packet as `achieved`
+        # priced in the same 72 algorithmic B/packet as `achieved`; --preimage: the pre-image
+        # kernel's probe build (vpcsum_pre_async bit 23: the same loads and 4-B stores, the stored
+        # sums written back unchanged), at 76 B/packet
+        def probe():
+            if pre:
+                V.pre(arena, d, pre_img, n, None, None, V.MODE_WRITE | 0x800000, V.PRE_FMT_PRE4, stream=stream)
+            else:
+                V.nat4_pattern_probe(arena, d, rw, n, stream=stream)
         for _ in range(3):
-            V.nat4_pattern_probe(arena, d, rw, n, stream=stream)
+            probe()
         e0.record(stream)
         for _ in range(10):
-            V.nat4_pattern_probe(arena, d, rw, n, stream=stream)
+            probe()
         e1.record(stream)
         pattern_ceiling = bytes_per_step / (e0.elapsed_ms(e1) / 10 * 1e-3) / 1e9
 
@@ -473,6 +520,15 @@ def main():
     # every line carries the CPU baseline, N > 1 included: rank 0 times it after the timed region
     # (the other ranks wait at the next collective), on rank 0's first packets
     cpu, gate = None, {}
+    if pre and n:
+        # the timed flushes applied the pre-images again and again: every rank's gate takes a fresh
+        # batch through one flush (then the descriptors lose F_PRE, for the verify below)
+        V.synth(arena, n, stride, 0, synth_id, SEED, first, d, stream=stream)
+        V.compute(arena, d, n, None, None, V.MODE_WRITE, stream=stream)
+        pre_img = prep_pre()
+        V.pre(arena, d, pre_img, n, None, None, V.MODE_WRITE, V.PRE_FMT_PRE4, stream=stream)
+        torch.cuda.synchronize()
+        d.view(n, 16)[:, 14] &= 0xFF ^ V.F_PRE
     if rank == 0 and not args.no_cpu_baseline and not nat and n:
         cpu, (m, want_out, want_st) = cpu_baseline(args.workload, synth_id, stride, first, args.cpu_budget)
         m = min(m, n)
@@ -508,11 +564,12 @@ def main():
 
     achieved = timed_bytes / args.steps / (kernel_ms * 1e-3) / 1e9 if n else 0.0
     # C5's summary: the 10M-packet pass with the bench's rewrite mask (src|dst|ports = 15)
-    traffic, traffic_src = pmc_traffic("nat15" if nat else args.workload, n) if args.team == 0 else (None, None)
+    traffic, traffic_src = pmc_traffic(("pre15" if pre else "nat15") if nat else args.workload, n) \
+        if args.team == 0 else (None, None)
     traffic_src = traffic_src or {}
     if rank == 0:
         value = total_bytes_step * args.steps / wall_max / 1e9
-        kname = "k_natq (RFC 1624)" if nat else "k_csum_d (K2)"
+        kname = ("k_pre (RFC 1624 from pre-images)" if pre else "k_natq (RFC 1624)") if nat else "k_csum_d (K2)"
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -569,7 +626,8 @@ def main():
                 "frac_of_pattern_ceiling": round(achieved / pattern_ceiling, 4) if pattern_ceiling else None,
                 "reference_order_probe_GBps": round(unit_order_ceiling, 1) if unit_order_ceiling else None,
                 "frac_of_reference_order_probe": round(achieved / unit_order_ceiling, 4) if unit_order_ceiling else None,
-                "pattern_ceiling_kernel": ("k_natq probe (same loads and stores, no rewrite)" if nat else
+                "pattern_ceiling_kernel": ("k_pre probe (same loads and stores, no arithmetic)" if pre else
+                                           "k_natq probe (same loads and stores, no rewrite)" if nat else
                                            "k_pattern_probe (K2's chunk reads, no checksum work)")
                 if pattern_ceiling else None,
                 "traffic_over_algorithmic": round(traffic / bytes_per_step, 3) if traffic and bytes_per_step else None,

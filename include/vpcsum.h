@@ -36,8 +36,12 @@ extern "C" {
 #endif
 
 /* 2 (round 4): VPCSUM_NAT_DEC_TTL refuses a TTL / hop limit <= 1 (S_BAD_DESC | S_TTL_EXPIRED)
- * instead of writing 0; vpcsum_synth_async takes a NULL arena (descriptors only). */
-#define VPCSUM_ABI_VERSION 2
+ * instead of writing 0; vpcsum_synth_async takes a NULL arena (descriptors only).
+ * 3 (round 5): VPCSUM_F_PRE and the pre-image entry points (vpcsum_pre_async,
+ * vpcsum_ctx_submit_pre, vpcsum_group_submit_pre, vpcsum_batch_submit_pre, VPCsum.submitPre);
+ * vpcsum_compute_async leaves F_PRE descriptors to vpcsum_pre_async; a handle of the process-wide
+ * group from before a vpcsum_shutdown is refused. */
+#define VPCSUM_ABI_VERSION 3
 
 /* ------------------------------------------------------------------------ */
 /* Data formats                                                             */
@@ -57,6 +61,15 @@ extern "C" {
                               * header).  VERIFY compares the stored field with that value.    */
 #define VPCSUM_F_RAW   0x04u /* Utils.calculateChecksum(buf, len) over [l3_off, l3_off+l3_len);
                                 result in out bits 0..15; nothing else is interpreted       */
+#define VPCSUM_F_PRE   0x10u /* with VPCSUM_F_L4 and / or F_IP: the packet was NAT'd by Java's
+                              * setters after its stored L4 sum was verified on ingress
+                              * (VPCSUM_S_L4_OK); its L4 sum is updated by RFC 1624 from the
+                              * packet's pre-image (vpcsum_pre_t: the words the setters
+                              * overwrote) instead of summed over the segment, its IPv4 header
+                              * sum recomputed.  Only the header is read.  Handled by
+                              * vpcsum_pre_async / vpcsum_ctx_submit_pre; vpcsum_compute_async
+                              * reads nothing of such a packet, writes nothing into its frame and
+                              * reports out 0 / S_DONE for it.                                 */
 
 typedef struct vpcsum_desc {
     uint64_t l3_off;   /* byte offset of the L3 (IP) header inside the arena               */
@@ -137,6 +150,17 @@ typedef struct vpcsum_nat4_rec {
 #define VPCSUM_NAT_STRICT_JAVA 0x01u /* rewrite, then full recompute: identical to Java for ANY
                                         input, including invalid input checksums              */
 
+/* Pre-image of a packet NAT'd by Java's own setters (VPCSUM_F_PRE): the OLD addresses and ports,
+ * recorded just before SwitchUtils.applyNat ran the setters (SwitchUtils.java:531-542), in the
+ * layout of the NAT entries: vpcsum_pre_t = vpcsum_nat_t (48 B; an IPv4 packet uses src[0..3] /
+ * dst[0..3]) and vpcsum_pre4_t = vpcsum_nat4_t (16 B, IPv4 only).  mask: VPCSUM_NAT_SRC / DST /
+ * SPORT / DPORT, the fields recorded (a field recorded but not changed adds nothing); the TTL
+ * bits and values are ignored: the IPv4 header sum is recomputed in full from the header. */
+typedef vpcsum_nat_t vpcsum_pre_t;
+typedef vpcsum_nat4_t vpcsum_pre4_t;
+#define VPCSUM_PRE_FMT_PRE4 0u   /* vpcsum_pre4_t entries */
+#define VPCSUM_PRE_FMT_PRE  1u   /* vpcsum_pre_t entries  */
+
 /* ------------------------------------------------------------------------ */
 /* Library / device                                                         */
 /* ------------------------------------------------------------------------ */
@@ -169,6 +193,20 @@ int vpcsum_nat_async(uint8_t* d_arena, uint64_t arena_len,
  * VPCSUM_NAT_RFC1624 only (the strict-Java recompute reads plain descriptors). */
 int vpcsum_nat4r_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_nat4_rec_t* d_rec, uint32_t n,
                        uint8_t* d_status, uint32_t nat_mode, void* stream);
+
+/* Egress sums of NAT'd packets from their pre-images: every descriptor with VPCSUM_F_PRE gets its
+ * L4 sum by RFC 1624 eqn. 3 from the stored field, the old words d_pre[i] records and the words now
+ * in the frame (HC' = ~(~HC + sum(~m + m'))), its IPv4 header sum (F_IP) recomputed in full from the
+ * header; a UDP stored 0 (no checksum) is summed in full.  The results equal Java's full recompute
+ * (getRawPacket(0) after the setters, AbstractPacket.java:15-22) whenever the stored L4 sum was
+ * correct before the rewrite -- what ingress verify's VPCSUM_S_L4_OK proves -- and nothing but the
+ * recorded fields changed since.  pre_fmt: VPCSUM_PRE_FMT_PRE4 (IPv4 only) or VPCSUM_PRE_FMT_PRE.
+ * mode: VPCSUM_MODE_WRITE to store the sums into the frames.  Out / status as vpcsum_compute_async
+ * (S_BAD_DESC: F_PRE without F_L4 or F_IP, with F_L4P / F_RAW, F_IP on IPv6, an IPv6 packet with
+ * 16-B entries, bounds).  d_pre holds n entries; those of descriptors without F_PRE are ignored.  Descriptors without F_PRE are not touched (out / status not written): run
+ * vpcsum_compute_async on the same batch first, on the same stream, for them. */
+int vpcsum_pre_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const void* d_pre,
+                     uint32_t pre_fmt, uint32_t n, uint32_t* d_out, uint8_t* d_status, uint32_t mode, void* stream);
 
 /* Build descriptors on the GPU by parsing Ethernet frames (EthernetPacket.from,
  * Ipv4Packet.from, Ipv6Packet.from rules). frame i = [d_frame_off[i], +d_frame_len[i]).
@@ -319,6 +357,16 @@ int vpcsum_ctx_egress_frames(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena
 int vpcsum_ctx_nat_submit(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena_len,
                           const vpcsum_desc_t* h_desc, const vpcsum_nat_t* h_rw, uint32_t n,
                           uint8_t* h_status, uint32_t nat_mode, uint64_t* ticket);
+/* The egress flush of a batch holding NAT'd frames: vpcsum_ctx_submit where
+ * descriptors with VPCSUM_F_PRE take their L4 sum from h_pre[i] (pre_fmt as vpcsum_pre_async;
+ * entries of other descriptors are ignored) and the others are summed in full, in one submission.
+ * Frames of a registered arena are read and written in place (an F_PRE packet: its header only);
+ * others are staged, an F_PRE packet's header only (its whole segment when it is UDP with a stored
+ * 0).  mode: VPCSUM_MODE_COMPUTE / VPCSUM_MODE_WRITE (not VERIFY).  Such batches are launched; the
+ * low-latency service grid takes plain batches only. */
+int vpcsum_ctx_submit_pre(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                          const void* h_pre, uint32_t pre_fmt, uint32_t n, uint32_t* h_out, uint8_t* h_status,
+                          uint32_t mode, uint64_t* ticket);
 /* Pipelined host->device->host throughput helper: processes a host arena of n fixed-stride
  * frames in `chunks` double-buffered pieces over two streams (H2D || kernel || D2H).  The arena,
  * descriptors and h_out must be registered (page-locked); with VPCSUM_MODE_WRITE the checksum
@@ -352,19 +400,29 @@ int vpcsum_group_wait(vpcsum_group_t* g, uint64_t ticket);
 int vpcsum_group_nat_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
                             const vpcsum_nat_t* h_rw, uint32_t n, uint8_t* h_status, uint32_t nat_mode,
                             uint64_t* ticket);
+/* as vpcsum_ctx_submit_pre, cut over the group's devices like vpcsum_group_submit */
+int vpcsum_group_submit_pre(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                            const void* h_pre, uint32_t pre_fmt, uint32_t n, uint32_t* h_out, uint8_t* h_status,
+                            uint32_t mode, uint64_t* ticket);
 
 /* ------------------------------------------------------------------------ */
 /* SURVEY.md §8(b)'s entry points: the same over ONE process-wide group.     */
 /* vpcsum_init(dev_mask) creates it (error if one exists), vpcsum_shutdown   */
 /* destroys it; the others fail with "vpcsum_init first" before it.  The     */
 /* handle of a submit is waited on with vpcsum_batch_wait (checksum and NAT  */
-/* batches alike).                                                           */
+/* batches alike).  vpcsum_shutdown first completes every batch still in     */
+/* flight (results delivered into the callers' buffers); a handle issued     */
+/* before it is then refused by vpcsum_batch_wait ("before vpcsum_shutdown"),*/
+/* also after a new vpcsum_init.                                             */
 /* ------------------------------------------------------------------------ */
 int vpcsum_init(uint64_t dev_mask, uint64_t max_arena_bytes, uint32_t max_pkts);
 int vpcsum_shutdown(void);
 int vpcsum_register_arena(void* h_arena, uint64_t len);
 int vpcsum_batch_submit(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, uint32_t n,
                         uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* handle);
+int vpcsum_batch_submit_pre(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, const void* h_pre,
+                            uint32_t pre_fmt, uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode,
+                            uint64_t* handle);
 int vpcsum_nat_submit(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, const vpcsum_nat_t* h_rw,
                       uint32_t n, uint8_t* h_status, uint32_t nat_mode, uint64_t* handle);
 int vpcsum_batch_wait(uint64_t handle);
@@ -418,6 +476,11 @@ int Java_io_vproxy_vpcsum_VPCsum_parseFrames(PNIEnv_vpcsum_long* env, int64_t ct
 int Java_io_vproxy_vpcsum_VPCsum_egressFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                               void* frameOff, void* frameLen, void* frameFlags, int32_t n, void* out,
                                               void* status);
+/* VPCsum.submitPre(long ctx, MemorySegment arena, long arenaLen, MemorySegment desc,
+ *                  MemorySegment pre, int n, MemorySegment out, MemorySegment status, int mode)
+ *   -> long ticket (vpcsum_ctx_submit_pre with 48-B vpcsum_pre_t entries) */
+int Java_io_vproxy_vpcsum_VPCsum_submitPre(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                           void* desc, void* pre, int32_t n, void* out, void* status, int32_t mode);
 /* VPCsum.natSubmit(long ctx, MemorySegment arena, long arenaLen, MemorySegment desc,
  *                  MemorySegment rw, int n, MemorySegment status, int natMode) -> long ticket */
 int Java_io_vproxy_vpcsum_VPCsum_natSubmit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,

@@ -39,6 +39,12 @@ import java.lang.foreign.ValueLayout;
  * verify overwrites it).  Copy what must outlive that, or pass your own segment to the overloads
  * that take one.
  *
+ * NAT'd frames (INTEGRATION.md §5): {@link PreImage#record} in SwitchUtils.applyNat keeps the old
+ * addresses / ports before the setters; {@link #defer} then marks the frame F_PRE when the ingress
+ * verify proved its stored L4 sum (PacketBuffer.csumStatus has S_L4_OK), and the flush updates its
+ * L4 sum from the pre-image reading only the header (VPCsum.submitPre).  Without that proof the
+ * frame is summed in full, like Java's getRawPacket(0).
+ *
  * {@link #stats} counts where every deferred frame went (GPU, small-flush hand-back, rejected
  * descriptor hand-back), next to IfaceStatistics: with INTEGRATION.md §3's diff the interface keeps
  * counting csum_skip for every frame whose sums Java left to someone else, the GPU included.
@@ -52,6 +58,8 @@ public final class GpuCsumBatch implements AutoCloseable {
     private final long umemLen;
     private final Arena arena = Arena.ofShared();
     private final MemorySegment desc;
+    private final MemorySegment pre;      // pre-images of the F_PRE frames (48 B per descriptor slot)
+    private int nPre = 0;                 // F_PRE frames in the pending descriptor batch
     private final MemorySegment out;
     private final MemorySegment status;
     private final int capacity;
@@ -74,11 +82,14 @@ public final class GpuCsumBatch implements AutoCloseable {
         public long smallFlushHandedBack;  // frames of flushes below SMALL_FLUSH, back to vpxdp
         public long badDescHandedBack;     // frames the kernel refused (S_BAD_DESC), back to vpxdp
         public long gpuFlushes;            // flushes that went to the GPU
+        public long preDeferred;           // NAT'd frames updated from their pre-image (F_PRE, header only)
+        public long preFull;               // NAT'd frames without a verified L4 sum: full recompute
 
         @Override
         public String toString() {
             return "csum_deferred=" + deferred + " csum_gpu=" + gpuHandled + " csum_small_flush=" + smallFlushHandedBack
-                   + " csum_bad_desc=" + badDescHandedBack + " csum_gpu_flushes=" + gpuFlushes;
+                   + " csum_bad_desc=" + badDescHandedBack + " csum_gpu_flushes=" + gpuFlushes
+                   + " csum_pre=" + preDeferred + " csum_pre_full=" + preFull;
         }
     }
 
@@ -96,9 +107,10 @@ public final class GpuCsumBatch implements AutoCloseable {
         this.umem = umem;
         this.umemLen = umem.byteSize();
         this.capacity = capacity;
-        if (VPCsum.get().abiVersion() != VPCsum.ABI_VERSION) {
-            throw new IOException("libvpcsum ABI " + VPCsum.get().abiVersion() + ", binding expects " + VPCsum.ABI_VERSION);
-        }
+        // before VPCsum is initialised (its PNI handles resolve in its static initialiser): a missing
+        // library or another ABI is an IOException here (VPCsum.ABI_VERSION is a constant: reading
+        // it does not initialise the class)
+        VPCsumLib.requireAbi(VPCsum.ABI_VERSION);
         this.ctx = VPCsum.get().create(env, device, umemLen, capacity);
         VPCsum.get().registerArena(env, ctx, umem, umemLen);
         // completeTx flushes are small: keep a resident GPU grid polling for them (20 ms idle).
@@ -106,6 +118,7 @@ public final class GpuCsumBatch implements AutoCloseable {
         // user of this GPU in this process waits up to 20 ms for it (INTEGRATION.md §7)
         VPCsum.get().setService(env, ctx, 20_000);
         this.desc = arena.allocate((long) DESC * capacity, 16);
+        this.pre = arena.allocate((long) VPCsum.PRE_ENTRY * capacity, 16);
         this.out = arena.allocate(4L * capacity, 16);
         this.status = arena.allocate(capacity, 16);
         this.chunks = new ChunkInfo[capacity];
@@ -192,6 +205,19 @@ public final class GpuCsumBatch implements AutoCloseable {
         if (n == capacity) {
             throw new IllegalStateException("batch full: flush first");
         }
+        // a NAT'd frame (PreImage.record ran in SwitchUtils.applyNat) whose stored L4 sum the
+        // ingress verify proved: its L4 sum is updated from the pre-image, only its header read
+        PreImage pi = pkb.csumPre;
+        if ((flags & VPCsum.F_L4) != 0 && pi != null && pi.isValid()) {
+            if (pkb.csumStatus >= 0 && (pkb.csumStatus & (VPCsum.S_L4_OK | VPCsum.S_BAD_DESC)) == VPCsum.S_L4_OK) {
+                flags |= VPCsum.F_PRE;
+                pi.writeTo(pre, (long) VPCsum.PRE_ENTRY * n);
+                ++nPre;
+                ++stats.preDeferred;
+            } else {
+                ++stats.preFull;
+            }
+        }
         long l3 = frameAddr + (((EthernetPacket) pkb.pkt).getVlan() >= 0 ? 18 : 14);
         // The lengths come from the IP header fields, never from the buffer: a frame parsed with
         // allowPartial (every XDP / tap frame, PacketBuffer.java:177 -> EthernetPacket.java:52-56)
@@ -277,9 +303,12 @@ public final class GpuCsumBatch implements AutoCloseable {
             }
             stats.smallFlushHandedBack += n;
             n = 0;
+            nPre = 0;
             return 0;
         }
-        long t = VPCsum.get().submit(env, ctx, umem, umemLen, desc, n, out, status, VPCsum.MODE_WRITE);
+        long t = nPre > 0 ? VPCsum.get().submitPre(env, ctx, umem, umemLen, desc, pre, n, out, status, VPCsum.MODE_WRITE)
+                          : VPCsum.get().submit(env, ctx, umem, umemLen, desc, n, out, status, VPCsum.MODE_WRITE);
+        nPre = 0;
         VPCsum.get().waitFor(env, ctx, t);
         for (int i = 0; i < n; ++i) {
             if ((status.get(ValueLayout.JAVA_BYTE, i) & VPCsum.S_BAD_DESC) != 0) {

@@ -4,11 +4,7 @@ import io.vproxy.pni.PNIEnv;
 import io.vproxy.pni.PNILinkOptions;
 import io.vproxy.pni.PanamaUtils;
 
-import java.lang.foreign.FunctionDescriptor;
-import java.lang.foreign.Linker;
 import java.lang.foreign.MemorySegment;
-import java.lang.foreign.SymbolLookup;
-import java.lang.foreign.ValueLayout;
 import java.lang.invoke.MethodHandle;
 
 /**
@@ -19,7 +15,7 @@ import java.lang.invoke.MethodHandle;
  * ENV).  The C side is include/vpcsum.h, symbols Java_io_vproxy_vpcsum_VPCsum_*.
  *
  * No method is linked critical ({@code setCritical(false)} throughout): every entry point may
- * block -- create / registerArena allocate and page-lock through the HIP runtime, submit /
+ * block -- create / registerArena allocate and page-lock through the HIP runtime, submit / submitPre /
  * natSubmit / verifyFrames / parseFrames finish the batch that last used their slot (an event wait, or the
  * service grid's completion), waitFor and setService wait by design.  A critical downcall keeps
  * the thread in Java state and would stall every safepoint (GC included) for that long.
@@ -39,20 +35,15 @@ public class VPCsum {
         return INSTANCE;
     }
 
-    /** include/vpcsum.h VPCSUM_ABI_VERSION this binding was written against (2: NAT_DEC_TTL refuses
-     * TTL <= 1 with S_TTL_EXPIRED).  {@link #abiVersion} reports the loaded library's. */
-    public static final int ABI_VERSION = 2;
+    /** include/vpcsum.h VPCSUM_ABI_VERSION this binding was written against (3: VPCSUM_F_PRE and
+     * submitPre; 2: NAT_DEC_TTL refuses TTL <= 1 with S_TTL_EXPIRED).  {@link #abiVersion} reports
+     * the loaded library's. */
+    public static final int ABI_VERSION = 3;
 
-    private static final MethodHandle abiVersionMH = Linker.nativeLinker().downcallHandle(
-        SymbolLookup.loaderLookup().find("vpcsum_abi_version").orElseThrow(), FunctionDescriptor.of(ValueLayout.JAVA_INT));
-
-    /** vpcsum_abi_version() of the loaded library (a plain C function, no PNIEnv). */
-    public int abiVersion() {
-        try {
-            return (int) abiVersionMH.invokeExact();
-        } catch (Throwable THROWABLE) {
-            throw new IllegalStateException("vpcsum_abi_version", THROWABLE);
-        }
+    /** vpcsum_abi_version() of the loaded library (a plain C function, no PNIEnv; {@link VPCsumLib}).
+     * Throws an IOException when libvpcsum is not loaded. */
+    public int abiVersion() throws java.io.IOException {
+        return VPCsumLib.abiVersion();
     }
 
     // descriptor flags (include/vpcsum.h)
@@ -61,6 +52,11 @@ public class VPCsum {
     public static final int F_RAW = 0x04;
     /** checksum offload (VP_CSUM_UP_PSEUDO): L4 field = folded pseudo-header sum (CHECKSUM_PARTIAL) */
     public static final int F_L4P = 0x08;
+    /** NAT'd packet whose stored L4 sum was verified on ingress: its L4 sum is updated from its
+     * pre-image (the old addresses / ports, {@link PreImage}) by RFC 1624 -- only the header is read */
+    public static final int F_PRE = 0x10;
+    /** bytes of one vpcsum_pre_t pre-image entry (the vpcsum_nat_t layout, old values) */
+    public static final int PRE_ENTRY = 48;
     // status bits
     public static final int S_IP_OK = 0x01;
     public static final int S_L4_OK = 0x02;
@@ -138,6 +134,31 @@ public class VPCsum {
         int ERR;
         try {
             ERR = (int) submitMH.invokeExact(ENV.MEMORY, ctx, arena, arenaLen, desc, n, out, status, mode);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+        return ENV.returnLong();
+    }
+
+    private static final MethodHandle submitPreMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
+        "Java_io_vproxy_vpcsum_VPCsum_submitPre", long.class /* ctx */, MemorySegment.class /* arena */,
+        long.class /* arenaLen */, MemorySegment.class /* desc */, MemorySegment.class /* pre */, int.class /* n */,
+        MemorySegment.class /* out */, MemorySegment.class /* status */, int.class /* mode */);
+
+    /** {@link #submit} for an egress batch that holds NAT'd frames: descriptors with F_PRE take their
+     * L4 sum from {@code pre[i]} (48-B vpcsum_pre_t, {@link PreImage#writeTo}) by RFC 1624, reading
+     * only the frame's header; the others are summed in full (vpcsum_ctx_submit_pre).  mode:
+     * MODE_COMPUTE or MODE_WRITE.  Returns a ticket for {@link #waitFor}. */
+    public long submitPre(PNIEnv ENV, long ctx, MemorySegment arena, long arenaLen, MemorySegment desc, MemorySegment pre,
+                          int n, MemorySegment out, MemorySegment status, int mode) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) submitPreMH.invokeExact(ENV.MEMORY, ctx, arena, arenaLen, desc, pre, n, out, status, mode);
         } catch (Throwable THROWABLE) {
             throw PanamaUtils.convertInvokeExactException(THROWABLE);
         }

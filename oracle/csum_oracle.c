@@ -252,19 +252,21 @@ void orc_process_batch(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
  * itself is single-threaded per Switch, Switch.java:170-199; N threads model N switches). */
 typedef struct {
     const uint8_t* arena; uint64_t arena_len; const vpcsum_desc_t* d; uint32_t lo, hi;
-    uint32_t mode; uint32_t* out; uint8_t* status;
+    uint32_t mode; uint32_t* out; uint8_t* status; uint8_t* arena_w;
 } orc_job;
 
 static void* orc_job_run(void* p) {
     orc_job* j = (orc_job*)p;
     for (uint32_t i = j->lo; i < j->hi; ++i)
         orc_process_one(j->arena, j->arena_len, j->d + i, j->mode, j->out ? j->out + i : NULL,
-                        j->status ? j->status + i : NULL, NULL);
+                        j->status ? j->status + i : NULL, j->arena_w);
     return NULL;
 }
 
-int orc_process_batch_mt(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, uint32_t n,
-                         uint32_t mode, uint32_t* out, uint8_t* status, int nthreads) {
+/* arena_w (MODE_WRITE): the packets of one batch must not overlap (test infrastructure: the
+ * threads write their own packets' fields) */
+int orc_process_batch_mt_w(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, uint32_t n,
+                           uint32_t mode, uint32_t* out, uint8_t* status, uint8_t* arena_w, int nthreads) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
@@ -273,19 +275,26 @@ int orc_process_batch_mt(const uint8_t* arena, uint64_t arena_len, const vpcsum_
         jobs[t].arena = arena; jobs[t].arena_len = arena_len; jobs[t].d = d;
         jobs[t].lo = (uint32_t)((uint64_t)n * t / nthreads);
         jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
-        jobs[t].mode = mode; jobs[t].out = out; jobs[t].status = status;
+        jobs[t].mode = mode; jobs[t].out = out; jobs[t].status = status; jobs[t].arena_w = arena_w;
         if (pthread_create(&th[t], NULL, orc_job_run, &jobs[t]) != 0) return -1;
     }
     for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
     return 0;
 }
 
+int orc_process_batch_mt(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, uint32_t n,
+                         uint32_t mode, uint32_t* out, uint8_t* status, int nthreads) {
+    return orc_process_batch_mt_w(arena, arena_len, d, n, mode, out, status, NULL, nthreads);
+}
+
 /* ---------------------------------------------------------------------------------------- */
 /* NAT / TTL rewrite restated as Java does it: setters, then a FULL recompute of the sums they */
 /* dirtied (SwitchUtils.applyNat SwitchUtils.java:522-542 -> getRawPacket(0)).               */
 /* ---------------------------------------------------------------------------------------- */
-void orc_nat_java(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const vpcsum_nat_t* rw,
-                  uint8_t* status) {
+/* The setters alone: returns 0 for a refused packet (status set, nothing written), else 1 with the
+ * sums they dirtied in *ip_dirty / *l4_dirty (AbstractPacket.checksumSkipped). */
+static int orc_nat_apply(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const vpcsum_nat_t* rw,
+                         uint8_t* status, int* ip_dirty_out, int* l4_dirty_out) {
     uint64_t off = d->l3_off;
     int ver = d->l3_ver, proto = d->l4_proto;
     uint32_t len = d->l3_len, l4o = d->l4_off;
@@ -295,14 +304,14 @@ void orc_nat_java(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, co
     else ok = 0;
     if (!ok) {
         if (status) *status = VPCSUM_S_BAD_DESC;
-        return;
+        return 0;
     }
     uint8_t* l3 = arena + off;
     /* IPInputRoute.java:81-88: hop <= 1 is dropped (ICMP time exceeded), never decremented */
     if ((rw->mask & VPCSUM_NAT_DEC_TTL) &&
         ((rw->mask & VPCSUM_NAT_SET_TTL) ? rw->ttl : l3[ver == 4 ? 8 : 7]) <= 1) {
         if (status) *status = VPCSUM_S_BAD_DESC | VPCSUM_S_TTL_EXPIRED;
-        return;
+        return 0;
     }
     int fld = orc_l4_field((uint32_t)proto);
     /* the L4 packet carries a checksum field (TcpPacket / UdpPacket / IcmpPacket) */
@@ -326,6 +335,20 @@ void orc_nat_java(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, co
         if (rw->mask & VPCSUM_NAT_SPORT) { memcpy(l3 + l4o, rw->sport, 2); l4_dirty = 1; }
         if (rw->mask & VPCSUM_NAT_DPORT) { memcpy(l3 + l4o + 2, rw->dport, 2); l4_dirty = 1; }
     }
+    *ip_dirty_out = ip_dirty;
+    *l4_dirty_out = l4_dirty;
+    return 1;
+}
+
+void orc_nat_java(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const vpcsum_nat_t* rw,
+                  uint8_t* status) {
+    int ip_dirty = 0, l4_dirty = 0;
+    if (!orc_nat_apply(arena, arena_len, d, rw, status, &ip_dirty, &l4_dirty)) return;
+    uint8_t* l3 = arena + d->l3_off;
+    uint32_t len = d->l3_len, l4o = d->l4_off;
+    int ver = d->l3_ver, proto = d->l4_proto;
+    int fld = orc_l4_field((uint32_t)proto);
+    /* getRawPacket(0): the dirty sums recomputed in full (AbstractPacket.java:15-22, 58-65) */
     if (ip_dirty) {
         uint32_t c = orc_ipv4_header_csum(l3, l4o);
         l3[10] = (uint8_t)(c >> 8); l3[11] = (uint8_t)c;
@@ -336,6 +359,19 @@ void orc_nat_java(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, co
         l3[l4o + fld] = (uint8_t)(c >> 8); l3[l4o + fld + 1] = (uint8_t)c;
     }
     if (status) *status = VPCSUM_S_DONE;
+}
+
+/* Java's setters alone, without the recompute: the new bytes in the frame, the stored sums as they
+ * were -- a NAT'd frame between SwitchUtils.applyNat (SwitchUtils.java:531-542) and its
+ * getRawPacket(0) at egress, the input of the pre-image flush (VPCSUM_F_PRE).  Status as
+ * orc_nat_java (S_DONE, or refused: nothing written).  Frames of one batch must not overlap. */
+void orc_nat_setters_batch(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d, const vpcsum_nat_t* rw,
+                           uint32_t n, uint8_t* status) {
+    for (uint32_t i = 0; i < n; ++i) {
+        int ip_dirty = 0, l4_dirty = 0;
+        if (orc_nat_apply(arena, arena_len, d + i, rw + i, status ? status + i : NULL, &ip_dirty, &l4_dirty) && status)
+            status[i] = VPCSUM_S_DONE;
+    }
 }
 
 /* The 16-B IPv4 entry: the same setters (rsv[0] = the SET_TTL value); IPv6 is rejected. */
@@ -501,4 +537,33 @@ void orc_synth_batch(uint8_t* arena, uint32_t n, uint32_t stride, uint32_t l3_pa
         orc_synth_frame(arena + (uint64_t)i * stride, l3_pad, workload, seed, first_index + i,
                         (uint64_t)i * stride, desc ? desc + i : NULL);
     }
+}
+
+/* The same split over threads (frames are independent). */
+typedef struct {
+    uint8_t* arena; uint32_t stride, l3_pad, workload; uint64_t seed, first; vpcsum_desc_t* desc; uint32_t lo, hi;
+} orc_synth_job;
+
+static void* orc_synth_job_run(void* p) {
+    orc_synth_job* j = (orc_synth_job*)p;
+    for (uint32_t i = j->lo; i < j->hi; ++i)
+        orc_synth_frame(j->arena + (uint64_t)i * j->stride, j->l3_pad, j->workload, j->seed, j->first + i,
+                        (uint64_t)i * j->stride, j->desc ? j->desc + i : NULL);
+    return NULL;
+}
+
+int orc_synth_batch_mt(uint8_t* arena, uint32_t n, uint32_t stride, uint32_t l3_pad, uint32_t workload,
+                       uint64_t seed, uint64_t first_index, vpcsum_desc_t* desc, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    orc_synth_job jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        orc_synth_job j = {arena, stride, l3_pad, workload, seed, first_index, desc,
+                           (uint32_t)((uint64_t)n * t / nthreads), (uint32_t)((uint64_t)n * (t + 1) / nthreads)};
+        jobs[t] = j;
+        if (pthread_create(&th[t], NULL, orc_synth_job_run, &jobs[t]) != 0) return -1;
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    return 0;
 }

@@ -30,7 +30,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "liborc.so")
 
-F_IP, F_L4, F_RAW, F_L4P = 0x01, 0x02, 0x04, 0x08
+F_IP, F_L4, F_RAW, F_L4P, F_PRE = 0x01, 0x02, 0x04, 0x08, 0x10   # F_PRE: Java recomputes in full
 S_IP_OK, S_L4_OK, S_UDP_NOCSUM, S_DONE, S_BAD_DESC = 0x01, 0x02, 0x04, 0x40, 0x80
 S_TTL_EXPIRED = 0x20
 MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
@@ -482,11 +482,16 @@ class Oracle:
         L.orc_csum_intermediate.argtypes = [U32, P, U32]
         L.orc_csum_intermediate.restype = U32
         L.orc_synth_batch.argtypes = [P, U32, U32, U32, U32, U64, U64, P]
+        L.orc_synth_batch_mt.argtypes = [P, U32, U32, U32, U32, U64, U64, P, ctypes.c_int]
+        L.orc_synth_batch_mt.restype = ctypes.c_int
+        L.orc_process_batch_mt_w.argtypes = [P, U64, P, U32, U32, P, P, P, ctypes.c_int]
+        L.orc_process_batch_mt_w.restype = ctypes.c_int
         L.orc_nat4_java.argtypes = [P, U64, P, P, P]
         L.orc_nat4_java_batch.argtypes = [P, U64, P, P, U32, P, ctypes.c_int]
         L.orc_nat4_java_batch.restype = ctypes.c_int
         L.orc_nat_java_batch.argtypes = [P, U64, P, P, ctypes.c_int, U32, P, ctypes.c_int]
         L.orc_nat_java_batch.restype = ctypes.c_int
+        L.orc_nat_setters_batch.argtypes = [P, U64, P, P, U32, P]
         L.orc_rng.argtypes = [U64, U64, U64]
         L.orc_rng.restype = U64
         self.L = L
@@ -506,19 +511,26 @@ class Oracle:
         status = np.zeros(n, np.uint8)
         if write:
             mode |= MODE_WRITE
-        if threads > 1 and not write:
-            rc = self.L.orc_process_batch_mt(self._p(arena), arena.nbytes, self._p(desc), n, mode,
-                                             self._p(out), self._p(status), threads)
+        if threads > 1:   # with write: the packets must not overlap
+            desc = np.ascontiguousarray(desc)
+            rc = self.L.orc_process_batch_mt_w(self._p(arena), arena.nbytes, self._p(desc), n, mode,
+                                               self._p(out), self._p(status), self._p(arena) if write else None,
+                                               threads)
             assert rc == 0
         else:
             self.L.orc_process_batch(self._p(arena), arena.nbytes, self._p(desc), n, mode,
                                      self._p(out), self._p(status), self._p(arena) if write else None)
         return out, status
 
-    def synth(self, n: int, stride: int, l3_pad: int, workload: int, seed: int, first_index: int = 0):
+    def synth(self, n: int, stride: int, l3_pad: int, workload: int, seed: int, first_index: int = 0,
+              threads: int = 1):
         arena = np.zeros(n * stride, np.uint8)
         desc = np.zeros(n, DESC_DTYPE)
-        self.L.orc_synth_batch(self._p(arena), n, stride, l3_pad, workload, seed, first_index, self._p(desc))
+        if threads > 1:
+            assert self.L.orc_synth_batch_mt(self._p(arena), n, stride, l3_pad, workload, seed, first_index,
+                                             self._p(desc), threads) == 0
+        else:
+            self.L.orc_synth_batch(self._p(arena), n, stride, l3_pad, workload, seed, first_index, self._p(desc))
         return arena, desc
 
     def nat4_java(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray, threads: int = 1):
@@ -540,6 +552,17 @@ class Oracle:
         rc = self.L.orc_nat_java_batch(self._p(arena), arena.nbytes, self._p(desc), self._p(rw), 1, len(desc),
                                        self._p(status), threads)
         assert rc == 0
+        return status
+
+    def nat_setters(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray):
+        """Java's setters alone (48-B entries): the new bytes written, the stored sums left stale --
+        the frames a pre-image flush (VPCSUM_F_PRE) receives.  Returns the status per packet."""
+        status = np.zeros(len(desc), np.uint8)
+        desc = np.ascontiguousarray(desc)
+        rw = np.ascontiguousarray(rw)
+        assert rw.dtype == NAT_DTYPE
+        self.L.orc_nat_setters_batch(self._p(arena), arena.nbytes, self._p(desc), self._p(rw), len(desc),
+                                     self._p(status))
         return status
 
     def rng(self, seed: int, pkt: int, word: int) -> int:

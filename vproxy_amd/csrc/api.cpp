@@ -327,6 +327,24 @@ int vpcsum_nat_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* 
     } VPC_CATCH("vpcsum_nat_async")
 }
 
+int vpcsum_pre_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const void* d_pre,
+                     uint32_t pre_fmt, uint32_t n, uint32_t* d_out, uint8_t* d_status, uint32_t mode, void* stream) {
+    try {
+        if (n == 0) return 0;
+        if (!d_arena || !d_desc || !d_pre) return fail("vpcsum_pre_async: NULL arena, descriptors or pre-images");
+        if (pre_fmt > VPCSUM_PRE_FMT_PRE) return fail("vpcsum_pre_async: bad pre_fmt %u", pre_fmt);
+        // tuning hints (not part of the stable ABI; nat.hip launch_pre): bit 8 byte accesses on the
+        // frames, bits 12..13 packets per lane (2: two; default one), bits 16..17 window chunks (2:
+        // four, 16-B entries only), bits 18..22 workgroups per CU, bit 23 the memory-pattern probe
+        // (16-B entries: the same loads and stores, the stored sums written back unchanged), bit 24
+        // non-temporal field stores
+        if (mode & ~(VPCSUM_MODE_WRITE | 0x100u | 0x3000u | 0x1ff0000u)) return fail("vpcsum_pre_async: bad mode 0x%x", mode);
+        VPC_CHECK(launch_pre(d_arena, arena_len, d_desc, d_pre, (int)pre_fmt, n, d_out, d_status, mode, (hipStream_t)stream),
+                  "vpcsum_pre_async launch");
+        return 0;
+    } VPC_CATCH("vpcsum_pre_async")
+}
+
 int vpcsum_parse_ether_async(const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_frame_off,
                              const uint32_t* d_frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* d_desc,
                              uint8_t* d_status, void* stream) {
@@ -560,15 +578,24 @@ int vpcsum_ctx_destroy(vpcsum_ctx_t* c) {
     try {
         if (!c) return 0;
         DeviceScope on_dev(c->device);
-        svc_free(c);
-        for (auto& s : c->slots) {
-            if (s.stream) (void)hipStreamSynchronize(s.stream);
-            slot_free(s);
+        int rc = 0;
+        {
+            std::lock_guard<std::mutex> lk(c->mu);
+            // batches still in flight complete first, as a wait would: their out / status (and a
+            // staged batch's frames) reach the caller's buffers before anything is freed.  A failure
+            // is reported, and the context is destroyed all the same.
+            for (auto& s : c->slots)
+                if (s.busy && slot_finish(c, s) != 0) rc = -1;
+            svc_free(c);
+            for (auto& s : c->slots) {
+                if (s.stream) (void)hipStreamSynchronize(s.stream);
+                slot_free(s);
+            }
+            for (auto& r : c->registered)
+                if (r.owned) (void)hipHostUnregister(r.host);
         }
-        for (auto& r : c->registered)
-            if (r.owned) (void)hipHostUnregister(r.host);
         delete c;
-        return 0;
+        return rc;
     } VPC_CATCH("vpcsum_ctx_destroy")
 }
 
@@ -755,6 +782,25 @@ static int slot_finish(vpcsum_ctx* c, Slot& s) {
     return 0;
 }
 
+// The slot's per-packet entry staging (NAT rewrites, pre-images: at most 48 B each), pinned and
+// mapped plus a device copy, allocated with the context's first batch that carries entries.
+static int slot_rw_alloc(vpcsum_ctx* c, Slot& s, const char* what) {
+    if (s.h_rw) return 0;
+    hipError_t e = hipSuccess;
+    const size_t bytes = (size_t)c->max_pkts * sizeof(vpcsum_nat_t);
+    if ((e = hipHostMalloc((void**)&s.h_rw, bytes, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&s.dh_rw, s.h_rw, 0)) != hipSuccess ||
+        (e = hipMalloc((void**)&s.d_rw, bytes)) != hipSuccess) {
+        if (s.h_rw) (void)hipHostFree(s.h_rw);
+        if (s.d_rw) (void)hipFree(s.d_rw);
+        s.h_rw = s.dh_rw = s.d_rw = nullptr;
+        return hipfail(e, what);
+    }
+    return 0;
+}
+
+static int l4_field_host(int proto) { return proto == 6 ? 16 : proto == 17 ? 6 : (proto == 1 || proto == 58) ? 2 : -1; }
+
 int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, uint32_t n,
                       uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket) {
     try {
@@ -914,6 +960,108 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
         *ticket = t;
         return 0;
     } VPC_CATCH("vpcsum_ctx_submit")
+}
+
+int vpcsum_ctx_submit_pre(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                          const void* h_pre, uint32_t pre_fmt, uint32_t n, uint32_t* h_out, uint8_t* h_status,
+                          uint32_t mode, uint64_t* ticket) {
+    try {
+        if (!c || !ticket) return fail("vpcsum_ctx_submit_pre: NULL context or ticket");
+        if (n > c->max_pkts) return fail("vpcsum_ctx_submit_pre: %u packets > capacity %u", n, c->max_pkts);
+        if (n && (!h_arena || !h_desc || !h_pre)) return fail("vpcsum_ctx_submit_pre: NULL arena, descriptors or pre-images");
+        if (pre_fmt > VPCSUM_PRE_FMT_PRE) return fail("vpcsum_ctx_submit_pre: bad pre_fmt %u", pre_fmt);
+        if (mode & ~VPCSUM_MODE_WRITE) return fail("vpcsum_ctx_submit_pre: bad mode 0x%x (COMPUTE or WRITE)", mode);
+        uint32_t npre = 0;
+        for (uint32_t i = 0; i < n; ++i) npre += (h_desc[i].flags & VPCSUM_F_PRE) ? 1u : 0u;
+        // no pre-image in the batch: a plain submit (the service grid may take it)
+        if (npre == 0) return vpcsum_ctx_submit(c, h_arena, arena_len, h_desc, n, h_out, h_status, mode, ticket);
+        const size_t esz = pre_fmt == VPCSUM_PRE_FMT_PRE ? sizeof(vpcsum_pre_t) : sizeof(vpcsum_pre4_t);
+        const bool full = npre < n;   // descriptors the checksum kernel sums in full
+        std::lock_guard<std::mutex> lk(c->mu);
+        VPC_ON_DEVICE(c->device);
+        const uint64_t t = c->next_ticket++;
+        Slot& s = c->slots[t & 1];
+        if (s.busy && slot_finish(c, s) != 0) return -1;
+        if (slot_rw_alloc(c, s, "vpcsum_ctx_submit_pre allocation") != 0) return -1;
+        memcpy(s.h_rw, h_pre, (size_t)n * esz);
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const vpcsum_desc_t& d = h_desc[i];
+            if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) continue;   // the kernels flag it BAD
+            lo = std::min(lo, d.l3_off);
+            hi = std::max(hi, d.l3_off + d.l3_len);
+        }
+        if (lo == UINT64_MAX) { lo = 0; hi = 0; }
+        lo &= ~(uint64_t)15;
+        uint8_t* dev_arena = hi > lo ? mapped_dev(c, h_arena + lo, hi - lo) : nullptr;
+        const uint32_t wr = mode & VPCSUM_MODE_WRITE;
+        if (dev_arena) {
+            // registered arena (umem): in place; an F_PRE packet's header is all that crosses PCIe
+            uint8_t* base = dev_arena - lo;
+            memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
+            if (full)
+                VPC_CHECK(launch_csum(base, arena_len, s.dh_desc, n, s.dh_out, s.dh_status, nullptr, VPCSUM_MODE_COMPUTE,
+                                      wr ? base : nullptr, n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
+                          "checksum launch (zero-copy)");
+            VPC_CHECK(launch_pre(base, arena_len, s.dh_desc, s.dh_rw, (int)pre_fmt, n, s.dh_out, s.dh_status, wr, s.stream),
+                      "pre-image launch (zero-copy)");
+            s.zero_copy = true;
+        } else {
+            // staged: each packet's 16-B blocks gathered into the pinned staging -- of an F_PRE
+            // packet only its header through the L4 checksum field (its descriptor's l3_len cut to
+            // that: the kernel reads no further), unless it is UDP with a stored 0, which is summed
+            // in full
+            uint64_t pos = 0;
+            for (uint32_t i = 0; i < n; ++i) {
+                const vpcsum_desc_t& d = h_desc[i];
+                s.h_desc[i] = d;
+                if (d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off) { s.h_desc[i].l3_off = UINT64_MAX; continue; }
+                uint32_t take = d.l3_len;
+                const int fld = l4_field_host(d.l4_proto);
+                if ((d.flags & VPCSUM_F_PRE) && fld >= 0 && (uint32_t)d.l4_off + fld + 2u <= d.l3_len) {
+                    const uint8_t* f = h_arena + d.l3_off + d.l4_off + fld;
+                    if (!(d.l4_proto == 17 && f[0] == 0 && f[1] == 0)) {
+                        take = std::max<uint32_t>(d.l3_ver == 4 ? 20u : 40u, (uint32_t)d.l4_off + fld + 2u);
+                        take = std::min<uint32_t>(take, d.l3_len);
+                        s.h_desc[i].l3_len = (uint16_t)take;
+                    }
+                }
+                const uint64_t a0 = d.l3_off & ~(uint64_t)15;
+                const uint64_t a1 = std::min<uint64_t>((d.l3_off + take + 15) & ~(uint64_t)15, arena_len);
+                if (pos + (a1 - a0) > c->max_arena) return fail("vpcsum_ctx_submit_pre: gathered batch exceeds capacity");
+                memcpy(s.h_arena + pos, h_arena + a0, a1 - a0);
+                s.h_desc[i].l3_off = pos + (d.l3_off - a0);
+                pos += (a1 - a0 + 15) & ~(uint64_t)15;
+            }
+            VPC_CHECK(hipMemcpyAsync(s.d_desc, s.h_desc, (size_t)n * sizeof(vpcsum_desc_t), hipMemcpyHostToDevice, s.stream),
+                      "H2D descriptors");
+            VPC_CHECK(hipMemcpyAsync(s.d_rw, s.h_rw, (size_t)n * esz, hipMemcpyHostToDevice, s.stream), "H2D pre-images");
+            if (pos) VPC_CHECK(hipMemcpyAsync(s.d_arena, s.h_arena, pos, hipMemcpyHostToDevice, s.stream), "H2D frames");
+            if (full)
+                VPC_CHECK(launch_csum(s.d_arena, pos, s.d_desc, n, s.d_out, s.d_status, nullptr, VPCSUM_MODE_COMPUTE, nullptr,
+                                      0, 0, s.stream),
+                          "checksum launch");
+            // the sums go back through out: slot_finish writes them into the caller's frames
+            VPC_CHECK(launch_pre(s.d_arena, pos, s.d_desc, s.d_rw, (int)pre_fmt, n, s.d_out, s.d_status, 0, s.stream),
+                      "pre-image launch");
+            VPC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream), "D2H out");
+            VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
+            s.zero_copy = false;
+        }
+        VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+        s.kind = 0;
+        s.svc_seq = 0;
+        s.busy = true;
+        s.ticket = t;
+        s.n = n;
+        s.mode = mode;
+        s.user_arena = h_arena;
+        s.user_desc = h_desc;
+        s.user_out = h_out;
+        s.user_status = h_status;
+        *ticket = t;
+        return 0;
+    } VPC_CATCH("vpcsum_ctx_submit_pre")
 }
 
 int vpcsum_ctx_wait(vpcsum_ctx_t* c, uint64_t ticket) {
@@ -1081,18 +1229,7 @@ int vpcsum_ctx_nat_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len,
         const uint64_t t = c->next_ticket++;
         Slot& s = c->slots[t & 1];
         if (s.busy && slot_finish(c, s) != 0) return -1;
-        if (!s.h_rw) {
-            hipError_t e = hipSuccess;
-            const size_t bytes = (size_t)c->max_pkts * sizeof(vpcsum_nat_t);
-            if ((e = hipHostMalloc((void**)&s.h_rw, bytes, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
-                (e = hipHostGetDevicePointer((void**)&s.dh_rw, s.h_rw, 0)) != hipSuccess ||
-                (e = hipMalloc((void**)&s.d_rw, bytes)) != hipSuccess) {
-                if (s.h_rw) (void)hipHostFree(s.h_rw);
-                if (s.d_rw) (void)hipFree(s.d_rw);
-                s.h_rw = s.dh_rw = s.d_rw = nullptr;
-                return hipfail(e, "vpcsum_ctx_nat_submit allocation");
-            }
-        }
+        if (slot_rw_alloc(c, s, "vpcsum_ctx_nat_submit") != 0) return -1;
         uint64_t lo = UINT64_MAX, hi = 0;
         for (uint32_t i = 0; i < n; ++i) {
             const vpcsum_desc_t& d = h_desc[i];
@@ -1294,10 +1431,19 @@ int vpcsum_group_create(uint64_t dev_mask, uint64_t max_arena_bytes, uint32_t ma
 int vpcsum_group_destroy(vpcsum_group_t* g) {
     try {
         if (!g) return 0;
-        for (auto* c : g->ctx) vpcsum_ctx_destroy(c);
+        int rc = 0;
+        {
+            // the group's batches in flight complete first (results into the callers' buffers);
+            // vpcsum_ctx_destroy does the same for anything submitted to a context directly
+            std::lock_guard<std::mutex> lk(g->mu);
+            for (auto& slot : g->slots)
+                if (slot.ticket && vpcsum_group_wait_locked(g, slot) != 0) rc = -1;
+        }
+        for (auto* c : g->ctx)
+            if (vpcsum_ctx_destroy(c) != 0) rc = -1;
         for (auto* h : g->reg) (void)hipHostUnregister(h);
         delete g;
-        return 0;
+        return rc;
     } VPC_CATCH("vpcsum_group_destroy")
 }
 
@@ -1436,6 +1582,22 @@ int vpcsum_group_nat_submit(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_
     } VPC_CATCH("vpcsum_group_nat_submit")
 }
 
+int vpcsum_group_submit_pre(vpcsum_group_t* g, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
+                            const void* h_pre, uint32_t pre_fmt, uint32_t n, uint32_t* h_out, uint8_t* h_status,
+                            uint32_t mode, uint64_t* ticket) {
+    try {
+        if (!g || !ticket) return fail("vpcsum_group_submit_pre: NULL group or ticket");
+        if (n && (!h_arena || !h_desc || !h_pre)) return fail("vpcsum_group_submit_pre: NULL arena, descriptors or pre-images");
+        if (pre_fmt > VPCSUM_PRE_FMT_PRE) return fail("vpcsum_group_submit_pre: bad pre_fmt %u", pre_fmt);
+        const size_t esz = pre_fmt == VPCSUM_PRE_FMT_PRE ? sizeof(vpcsum_pre_t) : sizeof(vpcsum_pre4_t);
+        std::lock_guard<std::mutex> lk(g->mu);
+        return group_submit_ranges(g, h_desc, n, ticket, [&](size_t d, uint32_t a, uint32_t b, uint64_t* t) {
+            return vpcsum_ctx_submit_pre(g->ctx[d], h_arena, arena_len, h_desc + a, (const uint8_t*)h_pre + a * esz, pre_fmt,
+                                         b - a, h_out ? h_out + a : nullptr, h_status ? h_status + a : nullptr, mode, t);
+        });
+    } VPC_CATCH("vpcsum_group_submit_pre")
+}
+
 int vpcsum_group_wait(vpcsum_group_t* g, uint64_t ticket) {
     try {
         if (!g) return fail("vpcsum_group_wait: NULL group");
@@ -1452,17 +1614,30 @@ int vpcsum_group_wait(vpcsum_group_t* g, uint64_t ticket) {
 // SURVEY.md §8(b)'s entry points over one process-wide device group (vpcsum_init creates it).
 // Every call on the group holds a shared lock for its whole duration and vpcsum_init /
 // vpcsum_shutdown an exclusive one: a shutdown on one thread waits for the submits and waits in
-// flight on others, and a call after it fails with "vpcsum_init first" (never a freed group).
+// flight on others and completes every batch still pending (vpcsum_group_destroy: results into
+// the callers' buffers); a call after it fails with "vpcsum_init first" (never a freed group).
+// A handle carries the generation of the group that issued it (bits 48..63; each vpcsum_init
+// starts a new one), so that a handle from before a shutdown is refused by the next group instead
+// of naming one of its tickets.
 }  // extern "C"
 
 static std::shared_mutex g_default_rw;
 static vpcsum_group* g_default = nullptr;
+static uint64_t g_default_gen = 0;   // generation of g_default (written under the exclusive lock)
+constexpr int kGenShift = 48;
+constexpr uint64_t kTicketMask = (1ull << kGenShift) - 1;
 
 template <class F>
 static int with_default_group(const char* what, F f) {
     std::shared_lock<std::shared_mutex> lk(g_default_rw);
     if (!g_default) return fail("%s: vpcsum_init first", what);
     return f(g_default);
+}
+
+// a submit's group ticket -> the handle the caller gets
+static int default_handle(int rc, uint64_t* handle) {
+    if (rc == 0 && handle) *handle = (*handle & kTicketMask) | (g_default_gen << kGenShift);
+    return rc;
 }
 
 extern "C" {
@@ -1474,6 +1649,7 @@ int vpcsum_init(uint64_t dev_mask, uint64_t max_arena_bytes, uint32_t max_pkts) 
         vpcsum_group_t* g = nullptr;
         if (vpcsum_group_create(dev_mask, max_arena_bytes, max_pkts, &g) != 0) return -1;
         g_default = g;
+        g_default_gen = (g_default_gen + 1) & 0xffff ? (g_default_gen + 1) & 0xffff : 1;
         return 0;
     } VPC_CATCH("vpcsum_init")
 }
@@ -1498,23 +1674,43 @@ int vpcsum_batch_submit(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_
                         uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* handle) {
     try {
         return with_default_group("vpcsum_batch_submit", [&](vpcsum_group* g) {
-            return vpcsum_group_submit(g, h_arena, arena_len, h_desc, n, h_out, h_status, mode, handle);
+            return default_handle(vpcsum_group_submit(g, h_arena, arena_len, h_desc, n, h_out, h_status, mode, handle),
+                                  handle);
         });
     } VPC_CATCH("vpcsum_batch_submit")
+}
+
+int vpcsum_batch_submit_pre(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, const void* h_pre,
+                            uint32_t pre_fmt, uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode,
+                            uint64_t* handle) {
+    try {
+        return with_default_group("vpcsum_batch_submit_pre", [&](vpcsum_group* g) {
+            return default_handle(vpcsum_group_submit_pre(g, h_arena, arena_len, h_desc, h_pre, pre_fmt, n, h_out, h_status,
+                                                          mode, handle),
+                                  handle);
+        });
+    } VPC_CATCH("vpcsum_batch_submit_pre")
 }
 
 int vpcsum_nat_submit(uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, const vpcsum_nat_t* h_rw,
                       uint32_t n, uint8_t* h_status, uint32_t nat_mode, uint64_t* handle) {
     try {
         return with_default_group("vpcsum_nat_submit", [&](vpcsum_group* g) {
-            return vpcsum_group_nat_submit(g, h_arena, arena_len, h_desc, h_rw, n, h_status, nat_mode, handle);
+            return default_handle(vpcsum_group_nat_submit(g, h_arena, arena_len, h_desc, h_rw, n, h_status, nat_mode, handle),
+                                  handle);
         });
     } VPC_CATCH("vpcsum_nat_submit")
 }
 
 int vpcsum_batch_wait(uint64_t handle) {
     try {
-        return with_default_group("vpcsum_batch_wait", [&](vpcsum_group* g) { return vpcsum_group_wait(g, handle); });
+        return with_default_group("vpcsum_batch_wait", [&](vpcsum_group* g) {
+            if ((handle >> kGenShift) != g_default_gen)
+                return fail("vpcsum_batch_wait: handle 0x%llx is from before vpcsum_shutdown (its batch was completed "
+                            "by the shutdown)",
+                            (unsigned long long)handle);
+            return vpcsum_group_wait(g, handle & kTicketMask);
+        });
     } VPC_CATCH("vpcsum_batch_wait")
 }
 
@@ -1634,6 +1830,23 @@ int Java_io_vproxy_vpcsum_VPCsum_parseFrames(PNIEnv_vpcsum_long* env, int64_t ct
         env->return_ = (int64_t)t;
         return 0;
     } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_parseFrames")
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_submitPre(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                           void* desc, void* pre, int32_t n, void* out, void* status, int32_t mode) {
+    try {
+        if (n < 0 || arenaLen < 0) {
+            fail("submitPre: negative size");
+            return pni_throw(env, "java.lang.IllegalArgumentException");
+        }
+        uint64_t t = 0;
+        if (vpcsum_ctx_submit_pre((vpcsum_ctx_t*)(intptr_t)ctx, (uint8_t*)arena, (uint64_t)arenaLen,
+                                  (const vpcsum_desc_t*)desc, pre, VPCSUM_PRE_FMT_PRE, (uint32_t)n, (uint32_t*)out,
+                                  (uint8_t*)status, (uint32_t)mode, &t) != 0)
+            return pni_throw(env, "java.io.IOException");
+        env->return_ = (int64_t)t;
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_submitPre")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_natSubmit(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,

@@ -76,4 +76,34 @@ __device__ __forceinline__ uint32_t buf_records(uint64_t arena_len) {
 __device__ __forceinline__ uint32_t ld16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
 __device__ __forceinline__ void st16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
 
+// Big-endian 16-bit store of a checksum field into a frame, non-temporal (written once; a plain
+// store of a partial line costs far more beside the nt read stream -- measured 2x on an
+// earlier team-per-packet kernel).
+__device__ __forceinline__ void st_be16_nt(uint8_t* p, uint32_t v) {
+    typedef __attribute__((address_space(1))) uint16_t g16;
+    typedef __attribute__((address_space(1))) uint8_t g8;
+    if (((uintptr_t)p & 1) == 0) {
+        __builtin_nontemporal_store((uint16_t)(((v & 0xff) << 8) | ((v >> 8) & 0xff)), (g16*)p);
+    } else {
+        __builtin_nontemporal_store((uint8_t)(v >> 8), (g8*)p);
+        __builtin_nontemporal_store((uint8_t)v, (g8*)(p + 1));
+    }
+}
+
+// The same with a plain store (written through L2: two fields of one line leave in one write-back).
+__device__ __forceinline__ void st_be16(uint8_t* p, uint32_t v) {
+    typedef __attribute__((address_space(1))) uint16_t g16;
+    typedef __attribute__((address_space(1))) uint8_t g8;
+    if (((uintptr_t)p & 1) == 0) {
+        *(g16*)p = (uint16_t)(((v & 0xff) << 8) | ((v >> 8) & 0xff));
+    } else {
+        *(g8*)p = (uint8_t)(v >> 8);
+        *(g8*)(p + 1) = (uint8_t)v;
+    }
+}
+
+// VPCSUM_F_PRE descriptors belong to the pre-image kernel (nat.hip k_pre): the checksum kernels
+// read none of their bytes and write nothing into their frames (flags 0: out 0, S_DONE).
+__device__ __forceinline__ int csum_flags(int fl) { return (fl & VPCSUM_F_PRE) ? 0 : fl; }
+
 }  // namespace vpcsum

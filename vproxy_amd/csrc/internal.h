@@ -48,6 +48,10 @@ hipError_t launch_nat(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* d
 // NAT's memory operations without the rewrite (tooling: the C5 pattern ceiling)
 hipError_t launch_nat_probe(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw, int fmt,
                             uint32_t n, hipStream_t stream);
+// pre-image egress sums (K6, VPCSUM_F_PRE descriptors only); fmt 0: vpcsum_pre4_t, 1: vpcsum_pre_t;
+// mode: VPCSUM_MODE_WRITE plus the tuning bits of vpcsum_pre_async
+hipError_t launch_pre(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* pre, int fmt, uint32_t n,
+                      uint32_t* out, uint8_t* status, uint32_t mode, hipStream_t stream);
 // strict mode, after the recompute: S_TTL_EXPIRED on the packets refused for their TTL
 hipError_t launch_nat_ttl_status(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* rw,
                                  int fmt, uint32_t n, uint8_t* status, hipStream_t stream);

@@ -97,6 +97,7 @@ __device__ __forceinline__ void k1_packet(const uint8_t* __restrict__ arena, uin
     const int proto = (dv.w >> 8) & 0xff;
     int fl = (dv.w >> 16) & 0xff;
     if (has_override) fl = fov;
+    fl = csum_flags(fl);
 
     // ---- validate (never read or write outside the arena) ----
     bool bad = off > arena_len || (uint64_t)len > arena_len - off || (fl & kFlagRejected);
@@ -133,7 +134,7 @@ __device__ __forceinline__ void k1_packet(const uint8_t* __restrict__ arena, uin
     pl.r0 = (int)((uintptr_t)l3 & 15);
     // pseudo-only (F_L4P): the IP header holds the pseudo addresses, the segment is not read
     const int need = psonly ? l4o + fld + 2 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
-    pl.nch = (pl.r0 + need + 15) >> 4;
+    pl.nch = need ? (pl.r0 + need + 15) >> 4 : 0;   // no sums (flags 0, F_PRE): nothing to read
     if (raw) {
         pl.l4lo = pl.r0; pl.l4hi = pl.r0 + len; pl.fa = -64;
         pl.fast_lo = (pl.r0 + 15) & ~15;
@@ -301,20 +302,6 @@ __device__ __forceinline__ void hdr_dword(uint32_t w, int d, const PktPlan& pl, 
     if (verify) {
         st_l4 += w & mf;
         st_ip += (w & mif) & (do_ip ? 0xffffffffu : 0u);
-    }
-}
-
-// Big-endian 16-bit store of a checksum field into a frame, non-temporal (written once; a plain
-// store of a partial line costs far more beside the nt read stream -- measured 2x on an
-// earlier team-per-packet kernel).
-__device__ __forceinline__ void st_be16_nt(uint8_t* p, uint32_t v) {
-    typedef __attribute__((address_space(1))) uint16_t g16;
-    typedef __attribute__((address_space(1))) uint8_t g8;
-    if (((uintptr_t)p & 1) == 0) {
-        __builtin_nontemporal_store((uint16_t)(((v & 0xff) << 8) | ((v >> 8) & 0xff)), (g16*)p);
-    } else {
-        __builtin_nontemporal_store((uint8_t)(v >> 8), (g8*)p);
-        __builtin_nontemporal_store((uint8_t)v, (g8*)(p + 1));
     }
 }
 
@@ -807,7 +794,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         const int l4o = dv.z >> 16;
         const int ver = dv.w & 0xff;
         const int proto = (dv.w >> 8) & 0xff;
-        const int fl = flags_override ? fov : (int)((dv.w >> 16) & 0xff);
+        const int fl = csum_flags(flags_override ? fov : (int)((dv.w >> 16) & 0xff));
 
         const int r0 = (int)(off & 15);
         // this lane's descriptor: set by the window check (one scalar check of lane 0's
@@ -975,7 +962,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
             const uint32_t boff = (uint32_t)(off & ~(uint64_t)15);
             // pseudo-only (F_L4P): the IP header holds the pseudo addresses, the segment is not read
             const int need = bad ? 0 : psonly ? l4o + fld + 2 : (raw || do_l4) ? len : (do_ip ? l4o : 0);
-            pl.nch = bad ? 0 : (r0 + need + 15) >> 4;
+            pl.nch = (bad || !need) ? 0 : (r0 + need + 15) >> 4;   // no sums (flags 0, F_PRE): no reads
             if (raw) {
                 pl.l4lo = r0; pl.l4hi = r0 + len; pl.fa = -64;
                 pl.fast_lo = (r0 + 15) & ~15;

@@ -196,18 +196,19 @@ __device__ uint32_t lane_sum_range(const uint8_t* lo_p, const uint8_t* hi_p, con
     return fold64(acc);
 }
 
-// Full UDP recompute from memory (the stored-0 case): pseudo header (IPv4 12..20 / IPv6 8..40,
-// proto 17, the L4 length as 16 / 32 bits) + the segment with the field excluded.
-__device__ void nat_udp_full(uint8_t* l3, int ver, int len, int l4o) {
-    uint8_t* l4p = l3 + l4o;
+// Full UDP sum from memory (the stored-0 case): pseudo header (IPv4 12..20 / IPv6 8..40, proto 17,
+// the L4 length as 16 / 32 bits) + the segment with the field excluded.
+__device__ uint32_t udp_full_sum(const uint8_t* l3, int ver, int len, int l4o) {
+    const uint8_t* l4p = l3 + l4o;
     const uint32_t seg = orient(lane_sum_range(l4p, l3 + len, l4p + 6), (int)((uintptr_t)l4p & 1));
     const uint32_t ps = orient(lane_sum_range(l3 + (ver == 4 ? 12 : 8), l3 + (ver == 4 ? 20 : 40), nullptr),
                                (int)((uintptr_t)l3 & 1));
     const uint32_t l4len = (uint32_t)(len - l4o);
     uint32_t c = 0xffff - fold32(seg + ps + 17u + (l4len & 0xffff) + (l4len >> 16));
     if (c == 0) c = 0xffff;
-    st16(l4p + 6, c);
+    return c;
 }
+__device__ void nat_udp_full(uint8_t* l3, int ver, int len, int l4o) { st16(l3 + l4o + 6, udp_full_sum(l3, ver, len, l4o)); }
 
 // Descriptor checks shared by both kernels; fmt 0 and 2 entries carry IPv4 addresses only.
 __device__ __forceinline__ bool nat_desc_ok(uint64_t off, int len, int l4o, int ver, uint64_t arena_len, int fmt) {
@@ -627,6 +628,273 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             for (int i = 0; i < W; ++i) store_bytes_packed(dst, p0 + i * T, n, res[i]);
         }
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// K6: egress sums of NAT'd packets from their pre-images (vpcsum_pre_async, VPCSUM_F_PRE).
+//
+// In the reference the rewrite is Java's: SwitchUtils.applyNat (SwitchUtils.java:531-542) calls
+// the setters, which write the new addresses / ports into the frame (raw.pktBuf.set, e.g.
+// Ipv4Packet.setSrc :433-445, TcpPacket.setSrcPort :31-40) and mark the sums dirty; the packet
+// then routes on the fields those setters cached (IPOutputRoute.java:52-53), and getRawPacket(0)
+// at egress recomputes every dirty sum over the whole segment (AbstractPacket.java:15-22, 58-65).
+// The vswitch keeps its setters and records, just before them, the old values (the pre-image);
+// at the egress flush the L4 sum is RFC 1624 eqn. 3 from the stored field, HC' = ~(~HC +
+// sum(~m + m')), m the recorded words, m' the words now in the frame -- nat_rfc1624's arithmetic
+// with the old words taken from the pre-image instead of the frame.  Bit-identical to the full
+// recompute when HC was correct (ingress verify's S_L4_OK, the caller's condition for F_PRE); a
+// UDP stored 0 is summed in full.  The IPv4 header sum is recomputed in full: its bytes are in
+// the window anyway.  Memory pattern: k_natq's quad-loaded header windows, minus the rewrite --
+// only the two sum fields are stored, 4 B per packet, by the owner lane.
+// ------------------------------------------------------------------------------------------
+
+// The F_PRE descriptor rules: F_L4 and / or F_IP, nothing else but F_PRE (no F_L4P / F_RAW), F_IP on
+// IPv4 only, nat_desc_ok's bounds and header rules (fmt 0, 16-B entries: IPv4 only), and with F_L4
+// an L4 checksum field inside the segment.
+__device__ __forceinline__ bool pre_desc_ok(const uint4 dv, uint64_t arena_len, int fmt) {
+    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+    const int len = dv.z & 0xffff, l4o = dv.z >> 16;
+    const int ver = dv.w & 0xff, proto = (dv.w >> 8) & 0xff, fl = (dv.w >> 16) & 0xff;
+    if ((fl & ~(VPCSUM_F_IP | VPCSUM_F_L4 | VPCSUM_F_PRE)) || !(fl & (VPCSUM_F_IP | VPCSUM_F_L4))) return false;
+    if ((fl & VPCSUM_F_IP) && ver != 4) return false;
+    return nat_desc_ok(off, len, l4o, ver, arena_len, fmt) && (!(fl & VPCSUM_F_L4) || nat_l4sum(ver, proto, len, l4o));
+}
+
+struct PreSums {
+    uint32_t ipc, l4c;
+    bool udp_full;   // UDP stored 0: the caller sums the segment (udp_full_sum)
+};
+
+// One packet's sums from its L3 header at l3 (its LDS window, or the frame on the byte path) and
+// its pre-image r.
+__device__ __forceinline__ PreSums pre_sums(const uint8_t* l3, int ver, int proto, int l4o, bool do_ip, bool do_l4,
+                                            const NatRw& r) {
+    PreSums o = {0u, 0u, false};
+    if (do_ip) {   // Ipv4Packet.__updateChecksum: the header, its own field as 0 (Ipv4Packet.java:209-217)
+        uint32_t s = 0;
+        for (int k = 0; k < l4o; k += 2)
+            if (k != 10) s += ld16(l3 + k);
+        o.ipc = 0xffff - fold32(s);
+    }
+    if (!do_l4) return o;
+    // the L4 sum's words a rewrite changes: the pseudo-header addresses of TCP / UDP and ICMPv6 (an
+    // ICMPv4 message has no pseudo header, inside IPv6 too) and the TCP / UDP ports (nat_setters)
+    const bool ports = proto == 6 || proto == 17;
+    const bool addr = ports || (ver == 6 && proto == 58);
+    uint32_t diff = 0;
+    // (constant trip counts: a runtime word index into the entry's registers would put it in scratch)
+    if (addr && ver == 4) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (r.mask & VPCSUM_NAT_SRC) diff += (~rw_word(r.src, k) & 0xffff) + ld16(l3 + 12 + 2 * k);
+            if (r.mask & VPCSUM_NAT_DST) diff += (~rw_word(r.dst, k) & 0xffff) + ld16(l3 + 16 + 2 * k);
+        }
+    } else if (addr) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (r.mask & VPCSUM_NAT_SRC) diff += (~rw_word(r.src, k) & 0xffff) + ld16(l3 + 8 + 2 * k);
+            if (r.mask & VPCSUM_NAT_DST) diff += (~rw_word(r.dst, k) & 0xffff) + ld16(l3 + 24 + 2 * k);
+        }
+    }
+    if (ports) {
+        if (r.mask & VPCSUM_NAT_SPORT) diff += (~rw_word(&r.ports, 0) & 0xffff) + ld16(l3 + l4o);
+        if (r.mask & VPCSUM_NAT_DPORT) diff += (~rw_word(&r.ports, 1) & 0xffff) + ld16(l3 + l4o + 2);
+    }
+    const uint32_t hc = ld16(l3 + l4o + l4_field(proto));
+    if (proto == 17 && hc == 0) {   // "no checksum": Java's recompute writes a real one (UdpPacket.java:136-164)
+        o.udp_full = true;
+        return o;
+    }
+    uint32_t c = ~fold32((~hc & 0xffff) + fold32(diff)) & 0xffff;
+    if (proto == 17 && c == 0) c = 0xffff;
+    o.l4c = c;
+    return o;
+}
+
+// Status bytes of the F_PRE lanes only (a mixed batch's other bytes are the checksum kernel's): a
+// quad of four such lanes stores one dword (as store_bytes_packed), the others byte by byte.
+__device__ __forceinline__ void store_bytes_masked(uint8_t* __restrict__ dst, uint32_t p, uint32_t n, uint32_t v, bool act) {
+    v &= 0xff;
+    const uint64_t am = __ballot(act);
+    const uint32_t b1 = (uint32_t)__shfl_down((int)v, 1, 64), b2 = (uint32_t)__shfl_down((int)v, 2, 64),
+                   b3 = (uint32_t)__shfl_down((int)v, 3, 64);
+    const int lane = threadIdx.x & 63;
+    if (((am >> (lane & ~3)) & 0xfull) == 0xfull) {
+        if ((lane & 3) == 0) {
+            const uint32_t packed = v | ((b1 & 0xff) << 8) | ((b2 & 0xff) << 16) | (b3 << 24);
+            if (p + 4 <= n && !((uintptr_t)(dst + p) & 3)) {
+                *(__attribute__((address_space(1))) uint32_t*)(dst + p) = packed;
+            } else {
+                for (uint32_t k = 0; k < 4 && p + k < n; ++k) dst[p + k] = (uint8_t)(packed >> (8 * k));
+            }
+        }
+    } else if (act) {
+        dst[p] = (uint8_t)v;
+    }
+}
+
+// FMT: entry format (0: vpcsum_pre4_t, 1: vpcsum_pre_t); W packets per lane and iteration; CH
+// window chunks (k_natq's); PROBE: the same loads and stores with no arithmetic -- the stored sums
+// are written back unchanged (tooling: the pattern ceiling of the pre-image flush).  byte_path: every
+// packet takes byte accesses on the frame (tests).
+template <int FMT, int W, int CH = kNatChunks, bool PROBE = false>
+__global__ __launch_bounds__(256) void k_pre(uint8_t* __restrict__ arena, uint64_t arena_len,
+                                            const uint4* __restrict__ desc, const void* __restrict__ pre, uint32_t n,
+                                            uint32_t* __restrict__ out, uint8_t* __restrict__ status, int write,
+                                            int byte_path, int nt_store) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const v4u gv4u;
+    constexpr int kSlotDw = 4 * CH + 1;   // LDS slot per packet: an odd dword stride
+    constexpr int NR = (CH + 3) / 4;       // quad rounds per window
+    __shared__ uint32_t s_win[256 * kSlotDw];
+    const int lane = threadIdx.x & 63;
+    uint32_t* wsl = &s_win[(threadIdx.x & ~63u) * kSlotDw];   // this wave's 64 slots
+    const uint8_t* w = (const uint8_t*)(wsl + lane * kSlotDw);
+    const uint32_t T = gridDim.x * blockDim.x;
+    const int ql = lane & 3;
+    for (uint32_t p0w = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); p0w < n; p0w += W * T) {
+        const uint32_t p0 = p0w + (uint32_t)lane;
+        uint4 dv[W];
+        NatRw rr[W];
+        bool act[W], ok[W];
+        uint32_t blo[W], bhi[W];   // window base (16-B aligned absolute address)
+        int wend[W];               // bytes of the window this packet needs; 0: none (byte path / idle)
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            dv[i] = p < n ? desc[p] : make_uint4(0, 0, 0, 0);
+            rr[i] = nat_load_rw<FMT>(pre, p < n ? p : 0);   // issued with the descriptor: independent of it
+        }
+        v4u v[W][4];
+        bool r2[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
+            const int l4o = dv[i].z >> 16;
+            const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
+            act[i] = p < n && (((dv[i].w >> 16) & 0xff) & VPCSUM_F_PRE) != 0;
+            ok[i] = act[i] && pre_desc_ok(dv[i], arena_len, FMT);
+            const uintptr_t la = ok[i] ? (uintptr_t)(arena + off) : 0;
+            const int r0 = (int)(la & 15);
+            const bool l4 = ((dv[i].w >> 16) & VPCSUM_F_L4) != 0;
+            const int need = max(ver == 4 ? 20 : 40, l4 ? l4o + l4_field(proto) + 2 : l4o);
+            wend[i] = ok[i] && !byte_path && r0 + need <= 16 * CH ? r0 + need : 0;
+            const uint64_t base = (uint64_t)(la - (uintptr_t)r0);
+            blo[i] = (uint32_t)base;
+            bhi[i] = (uint32_t)(base >> 32);
+            r2[i] = NR > 1 && __ballot(wend[i] > 64) != 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = 16 * u + (lane >> 2);
+                const uint32_t ql_lo = (uint32_t)__shfl((int)blo[i], q, 64);
+                const uint32_t ql_hi = (uint32_t)__shfl((int)bhi[i], q, 64);
+                const int qe = __shfl(wend[i], q, 64);
+                v4u x = {0u, 0u, 0u, 0u};
+                // only the chunks the packet needs, inside its 16-B blocks (never past a page)
+                if ((ql << 4) < qe) x = *(gv4u*)((((uint64_t)ql_hi << 32) | ql_lo) + 16u * (uint32_t)ql);
+                v[i][u] = x;
+            }
+        }
+        uint32_t res_out[W], res_st[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {   // stage the quads' chunks in the owners' slots
+                uint32_t* d = wsl + (16 * u + (lane >> 2)) * kSlotDw + 4 * ql;
+                d[0] = v[i][u].x; d[1] = v[i][u].y; d[2] = v[i][u].z; d[3] = v[i][u].w;
+            }
+            if (NR > 1 && r2[i]) {   // chunks 4.. of windows past 64 B (IPv4 options, IPv6)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int q = 16 * u + (lane >> 2);
+                    const uint32_t ql_lo = (uint32_t)__shfl((int)blo[i], q, 64);
+                    const uint32_t ql_hi = (uint32_t)__shfl((int)bhi[i], q, 64);
+                    const int qe = __shfl(wend[i], q, 64);
+                    const int k = 4 + ql;
+                    if (k < CH && (k << 4) < qe) {
+                        const v4u x = *(gv4u*)((((uint64_t)ql_hi << 32) | ql_lo) + 16u * (uint32_t)k);
+                        uint32_t* d = wsl + q * kSlotDw + 4 * k;
+                        d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            res_out[i] = 0;
+            res_st[i] = VPCSUM_S_BAD_DESC;
+            if (ok[i]) {
+                const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
+                const int len = dv[i].z & 0xffff, l4o = dv[i].z >> 16;
+                const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
+                const bool do_ip = ((dv[i].w >> 16) & VPCSUM_F_IP) != 0;
+                const bool do_l4 = ((dv[i].w >> 16) & VPCSUM_F_L4) != 0;
+                const int fld = l4_field(proto);
+                uint8_t* l3 = arena + off;
+                const int r0 = (int)((uintptr_t)l3 & 15);
+                PreSums s = {0u, 0u, false};
+                if (PROBE) {
+                    if (do_ip) s.ipc = ld16(w + r0 + 10);
+                    if (do_l4) s.l4c = ld16(w + r0 + l4o + fld);
+                } else {
+                    s = wend[i] ? pre_sums(w + r0, ver, proto, l4o, do_ip, do_l4, rr[i])
+                                : pre_sums(l3, ver, proto, l4o, do_ip, do_l4, rr[i]);
+                    if (s.udp_full) s.l4c = udp_full_sum(l3, ver, len, l4o);
+                }
+                if (write) {
+                    // plain stores: the two fields usually share a line, which L2 writes back once
+                    // (non-temporal ones reach DRAM apart: C5 12.6 vs 18.4 Gpps)
+                    if (nt_store) {
+                        if (do_ip) st_be16_nt(l3 + 10, s.ipc);
+                        if (do_l4) st_be16_nt(l3 + l4o + fld, s.l4c);
+                    } else {
+                        if (do_ip) st_be16(l3 + 10, s.ipc);
+                        if (do_l4) st_be16(l3 + l4o + fld, s.l4c);
+                    }
+                }
+                res_out[i] = (s.ipc & 0xffff) | ((s.l4c & 0xffff) << 16);
+                res_st[i] = VPCSUM_S_DONE;
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");   // the slots are rewritten for the next packet set
+        }
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint32_t p = p0 + i * T;
+            if (out && act[i]) out[p] = res_out[i];
+            if (status) store_bytes_masked(status, p, n, res_st[i], act[i]);
+        }
+    }
+}
+
+static uint32_t nat_grid(uint32_t n, int wl2, uint32_t wgs_per_cu);
+static uint32_t nat_wgs_per_cu(uint32_t nat_mode);
+
+hipError_t launch_pre(uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, const void* pre, int fmt, uint32_t n,
+                      uint32_t* out, uint8_t* status, uint32_t mode, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const int write = (mode & VPCSUM_MODE_WRITE) ? 1 : 0;
+    const int byte_path = (mode & 0x100u) ? 1 : 0;
+    // packets per lane: one by default (C5 +0.9% over two, profiles/r05d_presweep.json), bits 12..13 = 2: two
+    const int w1 = ((mode >> 12) & 3u) != 2;
+    const bool ch4 = ((mode >> 16) & 3u) == 2 && fmt == 0;       // 4-chunk windows (16-B entries only)
+    const bool probe = (mode & 0x800000u) != 0 && fmt == 0;
+    const int nt_store = (mode & 0x1000000u) ? 1 : 0;   // bit 24: non-temporal field stores (A/B)
+    const uint32_t g = nat_grid(n, w1 ? 0 : 1, nat_wgs_per_cu(mode));
+    const uint4* d = (const uint4*)desc;
+#define VPC_PRE(F, W, C, P)                                                                                             \
+    hipLaunchKernelGGL((k_pre<F, W, C, P>), dim3(g), dim3(256), 0, stream, arena, arena_len, d, pre, n, out, status, write, \
+                       byte_path, nt_store)
+    if (probe) {
+        if (ch4) VPC_PRE(0, 2, 4, true); else VPC_PRE(0, 2, kNatChunks, true);
+    } else if (fmt == 0) {
+        if (ch4) { if (w1) VPC_PRE(0, 1, 4, false); else VPC_PRE(0, 2, 4, false); }
+        else { if (w1) VPC_PRE(0, 1, kNatChunks, false); else VPC_PRE(0, 2, kNatChunks, false); }
+    } else {
+        if (w1) VPC_PRE(1, 1, kNatChunks, false); else VPC_PRE(1, 2, kNatChunks, false);
+    }
+#undef VPC_PRE
+    return hipGetLastError();
 }
 
 // Strict mode's status after the recompute kernel: that kernel reports a refused packet as

@@ -16,13 +16,14 @@ import numpy as np
 
 from .build import LIB
 
-F_IP, F_L4, F_RAW, F_L4P = 0x01, 0x02, 0x04, 0x08
+F_IP, F_L4, F_RAW, F_L4P, F_PRE = 0x01, 0x02, 0x04, 0x08, 0x10
 S_IP_OK, S_L4_OK, S_UDP_NOCSUM, S_DONE, S_BAD_DESC = 0x01, 0x02, 0x04, 0x40, 0x80
 S_TTL_EXPIRED = 0x20
 MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
 NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL, NAT_SET_TTL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 NAT_RFC1624, NAT_STRICT_JAVA = 0x00, 0x01
-ABI_VERSION = 2   # include/vpcsum.h VPCSUM_ABI_VERSION: the library this binding was written against
+PRE_FMT_PRE4, PRE_FMT_PRE = 0, 1   # pre-image entries: NAT4_DTYPE (16 B, IPv4) / NAT_DTYPE (48 B)
+ABI_VERSION = 3   # include/vpcsum.h VPCSUM_ABI_VERSION: the library this binding was written against
 SYNTH_C1, SYNTH_C2, SYNTH_C3, SYNTH_C4, SYNTH_FUZZ, SYNTH_C5 = 1, 2, 3, 4, 5, 6
 
 DESC_DTYPE = np.dtype([("l3_off", "<u8"), ("l3_len", "<u2"), ("l4_off", "<u2"), ("l3_ver", "u1"),
@@ -52,7 +53,8 @@ EXPORTS = [
     "vpcsum_group_create", "vpcsum_group_create_list", "vpcsum_group_destroy", "vpcsum_group_register_arena",
     "vpcsum_group_unregister_arena", "vpcsum_group_submit", "vpcsum_group_wait", "vpcsum_group_nat_submit",
     "vpcsum_init", "vpcsum_shutdown", "vpcsum_register_arena", "vpcsum_batch_submit", "vpcsum_nat_submit",
-    "vpcsum_batch_wait",
+    "vpcsum_batch_wait", "vpcsum_pre_async", "vpcsum_ctx_submit_pre", "vpcsum_group_submit_pre",
+    "vpcsum_batch_submit_pre", "Java_io_vproxy_vpcsum_VPCsum_submitPre",
     "Java_io_vproxy_vpcsum_VPCsum_create", "Java_io_vproxy_vpcsum_VPCsum_registerArena",
     "Java_io_vproxy_vpcsum_VPCsum_submit", "Java_io_vproxy_vpcsum_VPCsum_waitFor",
     "Java_io_vproxy_vpcsum_VPCsum_close", "Java_io_vproxy_vpcsum_VPCsum_setService",
@@ -85,6 +87,10 @@ def _declare(L):
         "vpcsum_nat4r_pattern_probe_async": ([P, U64, P, U32, P], I),
         "vpcsum_nat_async": ([P, U64, P, P, U32, P, U32, P], I),
         "vpcsum_ctx_nat_submit": ([P, P, U64, P, P, U32, P, U32, P], I),
+        "vpcsum_pre_async": ([P, U64, P, P, U32, U32, P, P, U32, P], I),
+        "vpcsum_ctx_submit_pre": ([P, P, U64, P, P, U32, U32, P, P, U32, P], I),
+        "vpcsum_group_submit_pre": ([P, P, U64, P, P, U32, U32, P, P, U32, P], I),
+        "vpcsum_batch_submit_pre": ([P, U64, P, P, U32, U32, P, P, U32, P], I),
         "vpcsum_group_create": ([U64, U64, U32, P], I),
         "vpcsum_group_create_list": ([P, I, U64, U32, P], I),
         "vpcsum_group_destroy": ([P], I),
@@ -201,6 +207,15 @@ def nat(arena, desc, rw, n: int, status=None, nat_mode: int = NAT_RFC1624, strea
                                   _stream(stream)), "vpcsum_nat_async")
 
 
+def pre(arena, desc, pre_img, n: int, out=None, status=None, mode: int = MODE_WRITE, pre_fmt: int = PRE_FMT_PRE4,
+        stream=None):
+    """vpcsum_pre_async: the sums of the F_PRE descriptors from their pre-images (`pre_img`: n
+    entries, NAT4_DTYPE bytes for PRE_FMT_PRE4 or NAT_DTYPE for PRE_FMT_PRE, holding the OLD
+    addresses / ports); descriptors without F_PRE are left alone (run `compute` for them first)."""
+    _check(lib().vpcsum_pre_async(_ptr(arena), arena.numel(), _ptr(desc), _ptr(pre_img), pre_fmt, n, _ptr(out),
+                                  _ptr(status), mode, _stream(stream)), "vpcsum_pre_async")
+
+
 def parse_ether(arena, frame_off, frame_len, n: int, desc, status=None, flags: int = F_IP | F_L4, stream=None,
                 tuples=None):
     """Descriptors from raw frames on the GPU; with `tuples` (n x 40 bytes, TUPLE_DTYPE) also each
@@ -308,6 +323,26 @@ class Context:
 
     def wait(self, ticket: int):
         _check(lib().vpcsum_ctx_wait(self.h, ticket), "vpcsum_ctx_wait")
+
+    def submit_pre(self, arena: np.ndarray, desc: np.ndarray, pre_img: np.ndarray, out: np.ndarray,
+                   status: np.ndarray | None = None, mode: int = MODE_COMPUTE) -> int:
+        """vpcsum_ctx_submit_pre: F_PRE descriptors take their L4 sum from pre_img[i] (NAT_DTYPE or
+        NAT4_DTYPE entries, old values), the others are summed in full; one submission."""
+        fmt = PRE_FMT_PRE if pre_img.dtype == NAT_DTYPE else PRE_FMT_PRE4
+        assert pre_img.dtype in (NAT_DTYPE, NAT4_DTYPE) and len(pre_img) >= len(desc)
+        t = ctypes.c_uint64()
+        _check(lib().vpcsum_ctx_submit_pre(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data,
+                                           pre_img.ctypes.data, fmt, len(desc), out.ctypes.data,
+                                           None if status is None else status.ctypes.data, mode, ctypes.byref(t)),
+               "vpcsum_ctx_submit_pre")
+        self._inflight[t.value & 1] = (arena, desc, pre_img, out, status)
+        return t.value
+
+    def run_pre(self, arena, desc, pre_img, mode: int = MODE_COMPUTE):
+        out = np.zeros(len(desc), np.uint32)
+        status = np.zeros(len(desc), np.uint8)
+        self.wait(self.submit_pre(arena, desc, pre_img, out, status, mode))
+        return out, status
 
     def verify_frames(self, arena: np.ndarray, frame_off: np.ndarray, frame_len: np.ndarray):
         """Ingress verify of received Ethernet frames in a registered arena: parsed and verified
@@ -436,6 +471,19 @@ class Group:
                                          out.ctypes.data, None if status is None else status.ctypes.data, mode,
                                          ctypes.byref(t)), "vpcsum_group_submit")
         self._inflight[t.value & 1] = (arena, desc, out, status)
+        return t.value
+
+    def submit_pre(self, arena: np.ndarray, desc: np.ndarray, pre_img: np.ndarray, out: np.ndarray,
+                   status: np.ndarray | None = None, mode: int = MODE_COMPUTE) -> int:
+        """vpcsum_group_submit_pre: Context.submit_pre cut over the group's devices."""
+        fmt = PRE_FMT_PRE if pre_img.dtype == NAT_DTYPE else PRE_FMT_PRE4
+        assert pre_img.dtype in (NAT_DTYPE, NAT4_DTYPE) and len(pre_img) >= len(desc)
+        t = ctypes.c_uint64()
+        _check(lib().vpcsum_group_submit_pre(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data,
+                                             pre_img.ctypes.data, fmt, len(desc), out.ctypes.data,
+                                             None if status is None else status.ctypes.data, mode, ctypes.byref(t)),
+               "vpcsum_group_submit_pre")
+        self._inflight[t.value & 1] = (arena, desc, pre_img, out, status)
         return t.value
 
     def nat_submit(self, arena: np.ndarray, desc: np.ndarray, rw: np.ndarray, status: np.ndarray | None = None,

@@ -105,6 +105,41 @@ def egress_descriptor(frame, frame_off: int, flags: int):
     return d
 
 
+NAT_FIELDS = V.NAT_SRC | V.NAT_DST | V.NAT_SPORT | V.NAT_DPORT
+
+
+def record_pre_image(arena, l3_off: int, ver: int, l4_off: int, proto: int, mask: int = NAT_FIELDS):
+    """The pre-image the vswitch records just before SwitchUtils.applyNat runs the setters
+    (SwitchUtils.java:531-542): the old source / destination address and, for
+    TCP / UDP, the old ports -- what ipPkt.getSrc() / getDst() and pkt.getSrcPort() / getDstPort()
+    return at that moment (the cached fields equal the frame's bytes: Ipv4Packet.from reads them
+    from the buffer, :73-145).  Returns one NAT_DTYPE record (vpcsum_pre_t) holding the old values,
+    mask = the fields recorded.  No checksum arithmetic happens here."""
+    e = np.zeros(1, V.NAT_DTYPE)[0]
+    a, alen = (l3_off + 12, 4) if ver == 4 else (l3_off + 8, 16)
+    if mask & V.NAT_SRC:
+        e["src"][:alen] = arena[a:a + alen]
+    if mask & V.NAT_DST:
+        e["dst"][:alen] = arena[a + alen:a + 2 * alen]
+    m = mask & (V.NAT_SRC | V.NAT_DST)
+    if proto in (6, 17):
+        p = l3_off + l4_off
+        if mask & V.NAT_SPORT:
+            e["sport"] = arena[p:p + 2]
+        if mask & V.NAT_DPORT:
+            e["dport"] = arena[p + 2:p + 4]
+        m |= mask & (V.NAT_SPORT | V.NAT_DPORT)
+    e["mask"] = m
+    return e
+
+
+def pre_eligible(rx_status: int) -> bool:
+    """Whether a NAT'd frame's L4 sum may be updated from its pre-image at egress: ingress verify
+    proved the stored L4 sum correct (S_L4_OK; a UDP stored 0 never carries it).  Otherwise the
+    frame takes the full recompute, as Java's getRawPacket(0) does (AbstractPacket.java:58-65)."""
+    return (rx_status & V.S_BAD_DESC) == 0 and (rx_status & V.S_L4_OK) != 0
+
+
 class EgressBatch:
     """Deferred egress checksums over one host frame arena (e.g. an AF_XDP umem).
 
@@ -129,6 +164,7 @@ class EgressBatch:
                 # flushes go to the persistent service grid instead of a launch each
                 self.ctx.set_service(service_idle_us)
         self.desc = np.zeros(capacity, V.DESC_DTYPE)
+        self.pre = np.zeros(capacity, V.NAT_DTYPE)   # pre-images of NAT'd frames (F_PRE), by slot
         self.out = np.zeros(capacity, np.uint32)
         self.status = np.zeros(capacity, np.uint8)
         self.n = 0
@@ -136,9 +172,10 @@ class EgressBatch:
         # INTEGRATION.md §3's diff (every frame whose sums Java left to someone else: the GPU or the
         # native path, XDPIface.java:117-120, 161-164); the rest say who took them.  Invariant:
         # deferred == gpu_handled + small_flush_handed_back + bad_desc_handed_back + pending.
+        # pre_deferred: frames whose L4 sum is updated from a pre-image (a subset of deferred).
         self.stats = {"tx_pkts": 0, "tx_csum_skip": 0, "deferred": 0, "gpu_handled": 0, "tx_csum_gpu": 0,
                       "small_flush_handed_back": 0, "bad_desc_handed_back": 0, "handed_back": 0, "rejected": 0,
-                      "flushes": 0}
+                      "flushes": 0, "pre_deferred": 0, "pre_full": 0}
 
     def _take(self, flags: int) -> bool:
         self.stats["tx_pkts"] += 1
@@ -147,12 +184,25 @@ class EgressBatch:
         self.stats["tx_csum_skip"] += 1
         return True
 
-    def defer(self, l3_off: int, l3_len: int, l4_off: int, ver: int, proto: int, flags: int) -> bool:
-        """Record a frame whose sums are dirty.  Returns False (nothing to do) when flags == 0."""
+    def defer(self, l3_off: int, l3_len: int, l4_off: int, ver: int, proto: int, flags: int,
+              pre=None, rx_status: int | None = None) -> bool:
+        """Record a frame whose sums are dirty.  Returns False (nothing to do) when flags == 0.
+
+        A NAT'd frame passes the `pre` image recorded before its setters ran
+        (:func:`record_pre_image`) and its ingress verify status: when that proved the stored L4
+        sum (:func:`pre_eligible`) the frame's L4 sum is updated from the pre-image (F_PRE: only its
+        header is read at the flush), otherwise it is recomputed in full (`pre_full`)."""
         if not self._take(flags):
             return False
         if self.n == self.capacity:
             self.complete_tx()
+        if pre is not None and flags & V.F_L4:
+            if rx_status is not None and pre_eligible(rx_status):
+                flags |= V.F_PRE
+                self.pre[self.n] = pre
+                self.stats["pre_deferred"] += 1
+            else:
+                self.stats["pre_full"] += 1
         self.desc[self.n] = (l3_off, l3_len, l4_off, ver, proto, flags, 0)
         self.n += 1
         self.stats["deferred"] += 1
@@ -187,7 +237,10 @@ class EgressBatch:
             self.stats["small_flush_handed_back"] += n
             self.n = 0
             return 0
-        t = self.ctx.submit(self.arena, self.desc[:n], self.out[:n], self.status[:n], V.MODE_WRITE)
+        if np.any(self.desc["flags"][:n] & V.F_PRE):
+            t = self.ctx.submit_pre(self.arena, self.desc[:n], self.pre[:n], self.out[:n], self.status[:n], V.MODE_WRITE)
+        else:
+            t = self.ctx.submit(self.arena, self.desc[:n], self.out[:n], self.status[:n], V.MODE_WRITE)
         self.ctx.wait(t)
         bad = (self.status[:n] & V.S_BAD_DESC) != 0
         nbad = int(np.count_nonzero(bad))
