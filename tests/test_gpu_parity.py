@@ -1101,6 +1101,17 @@ def test_verify_frames_rx_batch(V, orc):
     assert np.array_equal(out[ok], want_out[ok])
     assert np.array_equal(arena, before)                         # verify never writes frames
     assert int(np.sum(ok)) > 900 and int(np.sum((st & O.S_L4_OK) == 0)) > 100
+    # the seam's form (GpuCsumBatch.verifyFrames): no out words, the same status bytes
+    none, st2 = ctx.verify_frames(arena, np.array(offs), np.array(lens), sums=False)
+    assert none is None and np.array_equal(st2, want_st)
+    # and the descriptor form without out words, staged (a pageable copy) and zero-copy
+    infos = [O.parse_ether(f)[0] for f in frames]
+    dd = np.array([(offs[i] + x.l3_off, x.l3_len, x.l4_off, x.ver, x.proto, O.desc_flags_for(x), 0)
+                   for i, x in enumerate(infos) if x is not None], dtype=O.DESC_DTYPE)
+    for a in (arena, arena.copy()):
+        st3 = np.zeros(len(dd), np.uint8)
+        ctx.wait(ctx.submit(a, dd, None, st3, O.MODE_VERIFY))
+        assert np.array_equal(st3, want_st[ok])
     ctx.close()
 
 

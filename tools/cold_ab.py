@@ -24,6 +24,7 @@ ap.add_argument("--batches", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--iters", type=int, default=40)
 ap.add_argument("--mode", type=int, default=0, help="0 compute, 1 verify (status bytes written too)")
+ap.add_argument("--no-out", action="store_true", help="no out words (verify: the status bytes are the result)")
 ap.add_argument("--packets", type=int, default=0, help="packets per batch instead of the workload's")
 ap.add_argument("--bpc", default="0", help="workgroups per CU to try (0 = the launcher's choice)")
 args = ap.parse_args()
@@ -47,6 +48,7 @@ V.compute(arenas[1], descs[1], n, ref, None, 0, 4)
 for t, b in variants:   # every variant's results, once
     V.compute(arenas[1], descs[1], n, out, None, 0, t, blocks_per_cu=b)
     assert torch.equal(out, ref), f"variant {t} differs"
+o = None if args.no_out else out
 res = {(t, b, m): [] for t, b in variants for m in ("rotate", "repeat")}
 e0, e1 = V.Event(), V.Event()
 for r in range(args.rounds):
@@ -54,13 +56,14 @@ for r in range(args.rounds):
         for m in ("rotate", "repeat"):
             pick = (lambda i: i % nb) if m == "rotate" else (lambda i: 0)
             for i in range(nb):
-                V.compute(arenas[pick(i)], descs[pick(i)], n, out, st, args.mode, t, blocks_per_cu=b)
+                V.compute(arenas[pick(i)], descs[pick(i)], n, o, st, args.mode, t, blocks_per_cu=b)
             e0.record()
             for i in range(args.iters):
-                V.compute(arenas[pick(i)], descs[pick(i)], n, out, st, args.mode, t, blocks_per_cu=b)
+                V.compute(arenas[pick(i)], descs[pick(i)], n, o, st, args.mode, t, blocks_per_cu=b)
             e1.record()
             torch.cuda.synchronize()
             res[(t, b, m)].append(nbytes / (e0.elapsed_ms(e1) / args.iters) / 1e6)
-print(f"{text}, stride {stride}, {nb} batches of {n} packets: algorithmic {nbytes / n:.1f} B/pkt")
+print(f"{text}, stride {stride}, {nb} batches of {n} packets: algorithmic {nbytes / n:.1f} B/pkt, mode {args.mode}"
+      f"{', no out' if args.no_out else ''}")
 for (t, b, m), a in res.items():
     print(f"variant={t} bpc={b or 'def'} {m:6s}: median {np.median(a):7.1f} GB/s  max {max(a):7.1f}")

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-4 measurement call: GPU tests, bench lines of every config, kernel trace of the headline,
-# PMC passes (C2, C1, C3, NAT full / read-only / pattern probe), host path.  Every GPU step has its own time limit; a
-# crash / abort / timeout (exit > 1) ends the script.  usage: tools/gpu_r04.sh <tag> [parts]
+# Measurement call (rounds 4-5): GPU tests, bench lines of every config, kernel traces, PMC passes
+# (C2, C1, C3, C4, NAT full / read-only / pattern probe, the pre-image flush and its probe), host
+# path.  Every GPU step has its own time limit; a crash / abort / timeout (exit > 1) ends the
+# script.  usage: tools/gpu_measure.sh <tag> [parts]
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${1:-r04}; PARTS=${2:-tests,bench,trace,pmc,host}
@@ -32,6 +33,7 @@ if has bench; then
   for w in c1 c3 c4; do step bench_$w 300 python bench.py --workload $w --steps 200 --warmup 20; done
   step bench_c4_strong 300 python bench.py --workload c4 --strong --steps 200 --warmup 20 --no-cpu-baseline
   step bench_c5 400 python bench.py --workload c5 --steps 50 --warmup 5
+  step bench_c5pre 400 python bench.py --workload c5 --preimage --steps 50 --warmup 5
 fi
 if has trace; then
   step trace_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline
@@ -56,6 +58,17 @@ if has pmc || has pmcnat || has pmcnatprobe; then   # NAT's memory operations wi
   IFS='|' read -ra PS <<< "$N"; i=0
   for c in "${PS[@]}"; do i=$((i+1)); step pmc_natprobe_p$i 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_natprobe -o p$i -- python3 tools/prof_one.py --nat 0 --nat-mask 15 --nat-probe; done
   step trace_natprobe 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace_nat -o run -- python3 tools/prof_one.py --nat 0 --nat-mask 15 --nat-probe --iters 20
+fi
+if has pmc || has pmcpre; then   # the pre-image egress flush on C5 (bench --preimage's step) and its probe
+  N="FETCH_SIZE|WRITE_SIZE|TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum|SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES"
+  IFS='|' read -ra PS <<< "$N"; i=0
+  for c in "${PS[@]}"; do i=$((i+1)); step pmc_pre15_p$i 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_pre15 -o p$i -- python3 tools/prof_one.py --pre 0; done
+  i=0
+  for c in FETCH_SIZE WRITE_SIZE; do i=$((i+1)); step pmc_preprobe_p$i 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_preprobe -o p$i -- python3 tools/prof_one.py --pre 0x800000; done
+  step trace_c5pre 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace_c5pre -o run -- python3 bench.py --workload c5 --preimage --steps 50 --warmup 5 --no-cpu-baseline
+fi
+if has benchpre; then
+  step bench_c5pre 400 python bench.py --workload c5 --preimage --steps 50 --warmup 5
 fi
 if has pmc32; then   # last: a counter this gfx950 image may not have
   step pmc_nat15_p32 120 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/${TAG}_pmc_nat15 -o p32 -- python3 tools/prof_one.py --nat 0 --nat-mask 15

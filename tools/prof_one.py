@@ -14,7 +14,30 @@ ap.add_argument("--nat", type=int, default=-1, help="nat_mode: profile vpcsum_na
 ap.add_argument("--nat-mask", type=int, default=0x0F, help="rewrite mask of every entry (0: read-only pass)")
 ap.add_argument("--nat-n", type=int, default=10_000_000, help="C5 packets (BASELINE: 10M)")
 ap.add_argument("--nat-probe", action="store_true", help="the NAT pattern probe (same memory operations, no rewrite)")
+ap.add_argument("--pre", type=lambda x: int(x, 0), default=-1,
+                help="vpcsum_pre_async mode bits: profile the pre-image flush on C5 (bench --preimage's step)")
 a = ap.parse_args()
+if a.pre >= 0:
+    n, stride = a.nat_n, 2048
+    arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    V.synth(arena, n, stride, 0, V.SYNTH_C5, 0x20241020, 0, d)
+    V.compute(arena, d, n, None, None, V.MODE_WRITE)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    rw = torch.randint(0, 256, (n, 16), dtype=torch.uint8, generator=g).cuda()
+    fr = arena.view(n, stride)
+    p4 = torch.zeros((n, 16), dtype=torch.uint8, device="cuda")
+    p4[:, 0:8] = fr[:, 12:20]
+    p4[:, 8:12] = fr[:, 20:24]
+    p4[:, 12] = V.NAT_SRC | V.NAT_DST | V.NAT_SPORT | V.NAT_DPORT
+    fr[:, 12:20] = rw[:, 0:8]
+    fr[:, 20:24] = rw[:, 8:12]
+    d.view(n, 16)[:, 14] |= V.F_PRE
+    for _ in range(a.iters):
+        V.pre(arena, d, p4, n, None, None, V.MODE_WRITE | a.pre, V.PRE_FMT_PRE4)
+    torch.cuda.synchronize()
+    print("done")
+    sys.exit(0)
 if a.nat >= 0:
     n, stride = a.nat_n, 2048
     arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")

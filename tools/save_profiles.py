@@ -112,7 +112,7 @@ def resummarise(tag):
 def main(tag):
     os.makedirs(P, exist_ok=True)
     prov = provenance(tag)
-    for cfg in ("c2", "c1", "c3", "c4", "c4_strong", "c5", "c4s_8rank", "c5_8rank", "c2_2rank", "c5_2rank"):
+    for cfg in ("c2", "c1", "c3", "c4", "c4_strong", "c5", "c5pre", "c4s_8rank", "c5_8rank", "c2_2rank", "c5_2rank"):
         d = json_line(os.path.join(G, f"{tag}_bench_{cfg}.log"))
         if d:
             json.dump(d, open(os.path.join(P, f"{tag}_bench_{cfg}.json"), "w"), indent=1)
@@ -123,9 +123,13 @@ def main(tag):
         if not os.path.isdir(src):
             continue
         cfg = os.path.basename(src)[len(tag) + 5:]
-        nat = cfg.startswith("nat")
-        summarise(src, os.path.join(P, f"{tag}_pmc_{cfg}"), "vpcsum::k_nat" if nat else "k_csum",
-                  10_000_000 if nat else PACKETS[cfg], prov)
+        nat, pre = cfg.startswith("nat"), cfg.startswith("pre")
+        summarise(src, os.path.join(P, f"{tag}_pmc_{cfg}"), "vpcsum::k_pre" if pre else "vpcsum::k_nat" if nat else "k_csum",
+                  10_000_000 if nat or pre else PACKETS[cfg], prov)
+    for tr in ("nat", "c5pre"):   # kernel traces of the C5 commands
+        ks = os.path.join(G, f"{tag}_trace_{tr}", "run_kernel_stats.csv")
+        if os.path.exists(ks):
+            shutil.copy(ks, os.path.join(P, f"{tag}_{tr}_kernel_stats.csv"))
     d = json_line(os.path.join(G, f"{tag}_hostpath.log"))
     if d:
         json.dump(d, open(os.path.join(P, f"{tag}_hostpath_c2.json"), "w"), indent=1)

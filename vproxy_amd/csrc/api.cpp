@@ -898,7 +898,8 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
             // predicated loads), so the batch is a few PCIe round trips deep instead of K2's per-unit
             // iterations, and no chunk is read twice over PCIe
             const int variant = n <= kZeroCopyWaveTeams ? 12 : 0;
-            VPC_CHECK(launch_csum(base, arena_len, s.dh_desc, n, s.dh_out, s.dh_status, nullptr,
+            // no out words asked for (an ingress verify: the status bytes are the result): none written
+            VPC_CHECK(launch_csum(base, arena_len, s.dh_desc, n, h_out ? s.dh_out : nullptr, s.dh_status, nullptr,
                                   mode & VPCSUM_MODE_VERIFY, (mode & VPCSUM_MODE_WRITE) ? base : nullptr, variant, 0,
                                   s.stream),
                       "checksum launch (zero-copy)");
@@ -941,10 +942,13 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
                 }
                 VPC_CHECK(hipMemcpyAsync(s.d_arena, src, dev_len, hipMemcpyHostToDevice, s.stream), "H2D arena");
             }
-            VPC_CHECK(launch_csum(s.d_arena, dev_len, s.d_desc, n, s.d_out, s.d_status, nullptr, mode & VPCSUM_MODE_VERIFY,
-                                  nullptr, 0, 0, s.stream),
+            // the out words travel when the caller asked for them or MODE_WRITE places them in the frames
+            const bool want_out = h_out || (mode & VPCSUM_MODE_WRITE);
+            VPC_CHECK(launch_csum(s.d_arena, dev_len, s.d_desc, n, want_out ? s.d_out : nullptr, s.d_status, nullptr,
+                                  mode & VPCSUM_MODE_VERIFY, nullptr, 0, 0, s.stream),
                       "checksum launch");
-            VPC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream), "D2H out");
+            if (want_out)
+                VPC_CHECK(hipMemcpyAsync(s.h_out, s.d_out, (size_t)n * 4, hipMemcpyDeviceToHost, s.stream), "D2H out");
             VPC_CHECK(hipMemcpyAsync(s.h_status, s.d_status, n, hipMemcpyDeviceToHost, s.stream), "D2H status");
         }
         VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
@@ -1100,8 +1104,9 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
             VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.d_desc,
                                          nullptr, nullptr, s.stream),
                       "parse launch");
-            VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, s.dh_out, s.dh_status, nullptr, VPCSUM_MODE_VERIFY, nullptr,
-                                  n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
+            // h_out NULL: the status bytes alone (the out words are 4 of the 5 result bytes a packet writes)
+            VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, h_out ? s.dh_out : nullptr, s.dh_status, nullptr,
+                                  VPCSUM_MODE_VERIFY, nullptr, n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
                       "verify launch");
         }
         VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");

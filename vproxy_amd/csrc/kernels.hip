@@ -711,7 +711,14 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         const uint4 sd = desc[(uint32_t)(((uint64_t)n * (uint32_t)lane) >> 6)];
         if (__ballot((sd.z & 0xffffu) >= 1024u) == ~0ull) grid = low_grid;
         if (blk >= grid) return;   // whole workgroup, before any LDS use
-        if (WGS && !WIN && grid == gdim && n < 0xffff0000u) wg = __ballot((sd.z & 0xffffu) > 64u) != 0ull;
+        // sorted units only where the sample holds more than one cost class (a small packet,
+        // one trip, two trips, ... of the large tier): a uniform batch of mid-size packets keeps
+        // the per-wave units and their rotation
+        if (WGS && !WIN && grid == gdim && n < 0xffff0000u) {
+            const uint32_t len = sd.z & 0xffffu;
+            const uint32_t cls = len <= 64u ? 0u : 1u + (len + 15u) / (16u * kDefaultTeam * kDefaultUnroll);
+            wg = __ballot(cls != (uint32_t)__builtin_amdgcn_readfirstlane(cls)) != 0ull;
+        }
         if (!early && P0 + lo < n) {
             dnext = desc[P0 + lo];
             if (flags_override) fnext = flags_override[P0 + lo];

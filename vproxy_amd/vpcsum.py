@@ -312,11 +312,13 @@ class Context:
         _check(lib().vpcsum_ctx_unregister_arena(self.h, arr.ctypes.data), "vpcsum_ctx_unregister_arena")
         self._pinned.pop(arr.ctypes.data, None)
 
-    def submit(self, arena: np.ndarray, desc: np.ndarray, out: np.ndarray, status: np.ndarray | None = None,
+    def submit(self, arena: np.ndarray, desc: np.ndarray, out: np.ndarray | None, status: np.ndarray | None = None,
                mode: int = MODE_COMPUTE) -> int:
+        """out None: no out words (a verify whose result is the status bytes)."""
         t = ctypes.c_uint64()
         _check(lib().vpcsum_ctx_submit(self.h, arena.ctypes.data, arena.nbytes, desc.ctypes.data, len(desc),
-                                       out.ctypes.data, None if status is None else status.ctypes.data, mode,
+                                       None if out is None else out.ctypes.data,
+                                       None if status is None else status.ctypes.data, mode,
                                        ctypes.byref(t)), "vpcsum_ctx_submit")
         self._inflight[t.value & 1] = (arena, desc, out, status)
         return t.value
@@ -344,17 +346,19 @@ class Context:
         self.wait(self.submit_pre(arena, desc, pre_img, out, status, mode))
         return out, status
 
-    def verify_frames(self, arena: np.ndarray, frame_off: np.ndarray, frame_len: np.ndarray):
+    def verify_frames(self, arena: np.ndarray, frame_off: np.ndarray, frame_len: np.ndarray, sums: bool = True):
         """Ingress verify of received Ethernet frames in a registered arena: parsed and verified
-        on the GPU in one submission.  Returns (out, status) per frame."""
+        on the GPU in one submission.  Returns (out, status) per frame; sums=False: (None, status),
+        the kernel writes no out words (GpuCsumBatch.verifyFrames' form)."""
         n = len(frame_off)
         fo = np.ascontiguousarray(frame_off, dtype=np.uint64)
         fl = np.ascontiguousarray(frame_len, dtype=np.uint32)
-        out = np.zeros(n, np.uint32)
+        out = np.zeros(n, np.uint32) if sums else None
         status = np.zeros(n, np.uint8)
         t = ctypes.c_uint64()
         _check(lib().vpcsum_ctx_verify_frames(self.h, arena.ctypes.data, arena.nbytes, fo.ctypes.data, fl.ctypes.data,
-                                              n, out.ctypes.data, status.ctypes.data, ctypes.byref(t)),
+                                              n, None if out is None else out.ctypes.data, status.ctypes.data,
+                                              ctypes.byref(t)),
                "vpcsum_ctx_verify_frames")
         self.wait(t.value)
         return out, status
