@@ -1598,9 +1598,11 @@ def test_group_register_unregister_cycle(V, orc):
 
 def test_default_group_threads_race_shutdown(V, orc):
     """vpcsum_batch_submit / vpcsum_batch_wait from several threads while another thread shuts the
-    process-wide group down and re-initialises it: every call either completes with the oracle's
-    results or fails with "vpcsum_init first" -- never a use-after-free (the group is held
-    under a shared lock for each call, shutdown takes it exclusively)."""
+    process-wide group down and re-initialises it: never a use-after-free (the group is
+    held under a shared lock for each call, shutdown takes it exclusively), and every submit that
+    succeeded gets the oracle's results in its buffer, whether its wait returns 0 or a defined error:
+    "vpcsum_init first" (no group) or "before vpcsum_shutdown" (a handle of an earlier group) --
+    the shutdown completed the batch."""
     import ctypes
     import threading
     import torch
@@ -1608,7 +1610,7 @@ def test_default_group_threads_race_shutdown(V, orc):
     mask = 1
     arena, d = orc.synth(512, 2048, 14, O.SYNTH_C3, O.SEED, 2024)
     want, _ = orc.process(arena, d)
-    errors, done = [], [0]
+    errors, done, after_shutdown = [], [0], [0]
     stop = threading.Event()
 
     def worker():
@@ -1624,11 +1626,11 @@ def test_default_group_threads_race_shutdown(V, orc):
                 continue
             if L.vpcsum_batch_wait(h.value) != 0:
                 msg = L.vpcsum_last_error().decode()
-                if "vpcsum_init first" not in msg:
+                if "vpcsum_init first" not in msg and "before vpcsum_shutdown" not in msg:
                     errors.append(msg)
-                continue
+                after_shutdown[0] += 1
             if not np.array_equal(out, want):
-                errors.append("wrong results")
+                errors.append("a submitted batch's results were not delivered")
             done[0] += 1
 
     assert L.vpcsum_init(mask, arena.nbytes, len(d)) == 0
@@ -1647,6 +1649,44 @@ def test_default_group_threads_race_shutdown(V, orc):
     torch.cuda.synchronize()
     assert not errors, errors[:5]
     assert done[0] > 0
+
+
+def test_shutdown_completes_batches_and_refuses_old_handles(V, orc):
+    """vpcsum_shutdown completes every batch in flight before it frees anything (results in the
+    caller's buffers: staged and zero-copy), and a handle from before it is refused after a new
+    vpcsum_init instead of naming one of the new group's tickets."""
+    import ctypes
+    L = V.lib()
+    arena, d = orc.synth(700, 2048, 14, O.SYNTH_C3, O.SEED, 4040)
+    want, want_st = orc.process(arena, d)
+    for reg in (False, True):
+        assert L.vpcsum_init(1, arena.nbytes, len(d)) == 0
+        try:
+            if reg:
+                assert L.vpcsum_register_arena(arena.ctypes.data, arena.nbytes) == 0
+            outs = [np.zeros(len(d), np.uint32) for _ in range(2)]
+            sts = [np.zeros(len(d), np.uint8) for _ in range(2)]
+            hs = [ctypes.c_uint64() for _ in range(2)]
+            for o, st, h in zip(outs, sts, hs):   # two batches in flight, never waited
+                assert L.vpcsum_batch_submit(arena.ctypes.data, arena.nbytes, d.ctypes.data, len(d), o.ctypes.data,
+                                             st.ctypes.data, 0, ctypes.byref(h)) == 0
+        finally:
+            assert L.vpcsum_shutdown() == 0
+        for o, st in zip(outs, sts):
+            assert np.array_equal(o, want) and np.array_equal(st, want_st), reg
+        assert L.vpcsum_init(1, arena.nbytes, len(d)) == 0
+        try:
+            assert L.vpcsum_batch_wait(hs[1].value) != 0
+            assert "before vpcsum_shutdown" in L.vpcsum_last_error().decode()
+            h = ctypes.c_uint64()
+            out = np.zeros(len(d), np.uint32)
+            assert L.vpcsum_batch_submit(arena.ctypes.data, arena.nbytes, d.ctypes.data, len(d), out.ctypes.data,
+                                         None, 0, ctypes.byref(h)) == 0
+            assert (h.value & ((1 << 48) - 1)) == (hs[0].value & ((1 << 48) - 1))   # the same ticket number ...
+            assert h.value != hs[0].value                                            # ... of another generation
+            assert L.vpcsum_batch_wait(h.value) == 0 and np.array_equal(out, want)
+        finally:
+            L.vpcsum_shutdown()
 
 
 def test_full_size_c5_properties(V, orc):

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Where a kernel's time goes beyond HBM bytes (tooling): address translation (UTCL1), the TA / TCP
 # pipeline stalls and the SQ's VMEM issue FIFOs, per config.  One --pmc pass per line (gfx950 slots:
-# <= 4 TCP, 2 TA, 8 SQ).  usage: tools/pmc_deep.sh <tag> "<configs: c2 c3 c1 nat natprobe>"
+# <= 4 TCP, 2 TA, 8 SQ).  usage: tools/pmc_deep.sh <tag> "<configs: c2 c3 c1 nat natprobe c3_64 c3_576 c3_1500>"
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${1:-r03}; CFGS=${2:-"c2 c3 nat"}
@@ -13,6 +13,7 @@ for w in $CFGS; do
   case $w in
     nat) args="--nat 0 --nat-mask 15";;
     natprobe) args="--nat 0 --nat-mask 15 --nat-probe";;
+    c3_*) args="--workload c3 --class-len ${w#c3_}";;   # one C3 size class alone
     *) args="--workload $w";;
   esac
   i=0

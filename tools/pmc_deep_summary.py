@@ -8,7 +8,9 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PACKETS = {"c1": 1 << 20, "c2": 1 << 20, "c3": 1 << 20, "c4": 1 << 18, "nat": 10_000_000, "natprobe": 10_000_000}
+PACKETS = {"c1": 1 << 20, "c2": 1 << 20, "c3": 1 << 20, "c4": 1 << 18, "nat": 10_000_000, "natprobe": 10_000_000,
+           # C3's size classes in batch 0 (seed 0x20241020; tools/prof_one.py --class-len prints them)
+           "c3_64": 349686, "c3_576": 349183, "c3_1500": 349707}
 
 
 def main(tag, out_dir=None):
@@ -32,6 +34,10 @@ def main(tag, out_dir=None):
             out["utcl1_miss_rate"] = round(mean["TCP_UTCL1_TRANSLATION_MISS"] / mean["TCP_UTCL1_REQUEST"], 4)
         if mean.get("TCP_TCC_READ_REQ"):
             out["tcc_read_latency_cycles"] = round(mean.get("TCP_TCC_READ_REQ_LATENCY", 0) / mean["TCP_TCC_READ_REQ"], 1)
+        if mean.get("SQ_INSTS_VMEM_RD"):   # algorithmic bytes per vector-load instruction (1,024 at most: 64 x 16 B)
+            alg = {"c3_64": 84.0, "c3_576": 596.0, "c3_1500": 1520.0, "c3": 733.4, "c2": 1520.0, "c1": 84.0}.get(cfg)
+            if alg:
+                out["alg_bytes_per_vmem_rd"] = round(alg * n / mean["SQ_INSTS_VMEM_RD"], 1)
         if mean.get("SQ_WAVE_CYCLES"):
             for k in ("SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_VMEM_TA_CMD_FIFO_FULL",
                       "SQ_ACTIVE_INST_VMEM"):

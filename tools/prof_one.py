@@ -14,6 +14,7 @@ ap.add_argument("--nat", type=int, default=-1, help="nat_mode: profile vpcsum_na
 ap.add_argument("--nat-mask", type=int, default=0x0F, help="rewrite mask of every entry (0: read-only pass)")
 ap.add_argument("--nat-n", type=int, default=10_000_000, help="C5 packets (BASELINE: 10M)")
 ap.add_argument("--nat-probe", action="store_true", help="the NAT pattern probe (same memory operations, no rewrite)")
+ap.add_argument("--class-len", type=int, default=0, help="only the workload's packets of this L3 length (C3 classes)")
 ap.add_argument("--pre", type=lambda x: int(x, 0), default=-1,
                 help="vpcsum_pre_async mode bits: profile the pre-image flush on C5 (bench --preimage's step)")
 a = ap.parse_args()
@@ -62,6 +63,12 @@ sid, n, stride, _ = WORKLOADS[a.workload]
 arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
 d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
 V.synth(arena, n, stride, 0, sid, 0x20241020, 0, d)
+if a.class_len:   # a size class of the batch alone (same arena, descriptor subset)
+    desc = V.tensor_to_desc(d)
+    sub = desc[desc["l3_len"] == a.class_len]
+    n = len(sub)
+    d = V.desc_to_tensor(sub)
+    print("packets", n)
 out = torch.zeros(n, dtype=torch.int32, device="cuda")
 st = torch.zeros(n, dtype=torch.uint8, device="cuda") if a.mode == 1 else None
 for v in map(int, a.variants.split(",")):
