@@ -103,4 +103,14 @@ if has rank2; then   # the multi-rank path rehearsed on one GPU (bench.py launch
   step bench_c2_2rank 300 python bench.py --gpus 2 --steps 50 --warmup 5 --no-cpu-baseline --share-gpu
   step bench_c5_2rank 400 python bench.py --workload c5 --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline --share-gpu
 fi
+if has preflush; then   # the NAT'd 1024-frame host flush, pre-image vs full recompute
+  step preflush 300 python tools/preflush.py
+fi
+if has c3split; then   # C3 per size class: K2, unsorted, verify, grid / unit-order probes
+  step c3split 300 python tools/c3_split.py
+  step c3var 400 python tools/c3_variants.py --variants 0,79,78
+fi
+if has verify; then   # compute vs verify (out + status) vs status-only verify, uncached
+  step verify 900 bash tools/verify_modes.sh ${TAG}_vm "c1 c3 c2" ${VM_ROUNDS:-2}
+fi
 echo ALLDONE

@@ -139,6 +139,18 @@ def main(tag):
         if rows:
             json.dump({"src_hash": prov["src_hash"], "head": prov["head"], "rows": rows},
                       open(os.path.join(P, f"{tag}_flush_latency.json"), "w"), indent=1)
+    for name, out in (("preflush", "preflush"), ("c3split", "c3split"), ("c3var", "c3_variants")):
+        d = json_line(os.path.join(G, f"{tag}_{name}.log"))
+        if d:
+            json.dump({"src_hash": prov["src_hash"], "head": prov["head"], **d},
+                      open(os.path.join(P, f"{tag}_{out}.json"), "w"), indent=1)
+    vm = sorted(glob.glob(os.path.join(G, f"{tag}_vm_*.log")))   # tools/verify_modes.sh logs
+    if vm:
+        dst = os.path.join(P, f"{tag}_verify_modes")
+        os.makedirs(dst, exist_ok=True)
+        for f in vm:
+            shutil.copy(f, dst)
+        json.dump({"src_hash": prov["src_hash"], "head": prov["head"]}, open(os.path.join(dst, "src.json"), "w"))
     print("saved", sorted(f for f in os.listdir(P) if f.startswith(tag)))
 
 
