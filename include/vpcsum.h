@@ -362,8 +362,10 @@ int vpcsum_ctx_nat_submit(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena_le
  * entries of other descriptors are ignored) and the others are summed in full, in one submission.
  * Frames of a registered arena are read and written in place (an F_PRE packet: its header only);
  * others are staged, an F_PRE packet's header only (its whole segment when it is UDP with a stored
- * 0).  mode: VPCSUM_MODE_COMPUTE / VPCSUM_MODE_WRITE (not VERIFY).  Such batches are launched; the
- * low-latency service grid takes plain batches only. */
+ * 0).  mode: VPCSUM_MODE_COMPUTE / VPCSUM_MODE_WRITE (not VERIFY).  A batch of up to 512 packets
+ * from a registered arena goes to the low-latency service grid when it is on
+ * (vpcsum_ctx_set_service), F_PRE frames and the others together; larger ones are launched.  The
+ * entries' rsv bytes are ignored. */
 int vpcsum_ctx_submit_pre(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc,
                           const void* h_pre, uint32_t pre_fmt, uint32_t n, uint32_t* h_out, uint8_t* h_status,
                           uint32_t mode, uint64_t* ticket);

@@ -20,3 +20,14 @@ def orc():
     from oracle import oracle as O
     O.build()
     return O.Oracle()
+
+
+@pytest.fixture(autouse=True)
+def _sync_after_gpu_test(request):
+    """VPCSUM_SYNC_EACH_TEST=1 (debugging): synchronise the device after every GPU test, so that a
+    fault from asynchronous work (a service grid still polling, a kernel on another stream) is
+    reported against the test that started it, not the next one."""
+    yield
+    if os.environ.get("VPCSUM_SYNC_EACH_TEST") == "1" and request.node.get_closest_marker("gpu"):
+        import torch
+        torch.cuda.synchronize()

@@ -118,25 +118,29 @@ def test_egress_rejected_descriptor_is_handed_back(V, orc):
 
 
 @pytest.mark.gpu
-def test_egress_frames_parsed_on_gpu(V, orc):
+@pytest.mark.parametrize("service", [False, True])
+def test_egress_frames_parsed_on_gpu(V, orc, service):
     """vpcsum_ctx_egress_frames (FrameEgressBatch / VPCsum.egressFrames): only the frame offsets,
     the frame lengths as the TX ring sends them (padding and trailers included) and per-frame flags
-    go to the GPU, which places L3 / L4 itself.  The umem equals the oracle's full recompute of
-    the same frames, byte for byte."""
+    go to the GPU, which places L3 / L4 itself (a parse kernel and a checksum kernel, or the service
+    grid's parse + sum per frame).  The umem equals the oracle's full recompute of the same frames,
+    byte for byte."""
     from vproxy_amd import vswitch as S
     fs, arena, offs, flags = _batch()
     want = arena.copy()
     orc.process(want, E.oracle_descriptors(fs, offs, flags), O.MODE_COMPUTE, write=True)
-    b = S.FrameEgressBatch(arena, capacity=len(fs))
+    b = S.FrameEgressBatch(arena, capacity=len(fs), service_idle_us=20000 if service else 0)
     for f, o, fl in zip(fs, offs, flags):
         assert b.defer(o, len(f["frame"]), fl)
     assert b.complete_tx() == len(fs) and not b.handed_back
     assert np.array_equal(arena, want)
+    assert b.ctx.stats()["service_batches"] == (1 if service else 0)
     b.close()
 
 
 @pytest.mark.gpu
-def test_egress_frames_refusals(V, orc):
+@pytest.mark.parametrize("service", [False, True])
+def test_egress_frames_refusals(V, orc, service):
     """Frames the GPU cannot honour are refused whole -- S_BAD_DESC, nothing written -- and handed
     back: an IPv4 header sum asked of IPv6, a pseudo-header sum asked of ICMPv4 (it has none), an
     ARP frame, a frame cut inside its IPv4 header, F_L4 and F_L4P together, F_RAW.  The others of
@@ -159,13 +163,53 @@ def test_egress_frames_refusals(V, orc):
     want = arena.copy()
     orc.process(want, E.oracle_descriptors([fs[i] for i in good], [offs[i] for i in good],
                                            [flags[i] for i in good]), O.MODE_COMPUTE, write=True)
-    b = S.FrameEgressBatch(arena, capacity=len(fs))
+    b = S.FrameEgressBatch(arena, capacity=len(fs), service_idle_us=20000 if service else 0)
     for o, L, fl in zip(offs, lens, flags):
         b.defer(o, L, fl)
     assert b.complete_tx() == len(good)
     assert sorted(x[0] for x in b.handed_back) == sorted(offs[i] for i in bad)
     assert np.array_equal(arena, want)
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("idle_us", [5000, 40])
+def test_egress_frames_service_flushes(V, orc, idle_us):
+    """Raw-frame flushes of 1..512 frames through the service grid (svc_frame_packet: each frame's
+    first 384 B staged, parsed by lane 0, summed by the wave), consecutive batches over the 220
+    vector frames (802.1Q, IPv4 options, IPv6 extension headers, padding, trailers) and a random
+    stream, some frames refused (an ARP EtherType, flags a frame cannot honour): every status and
+    every byte of the umem equals the launched path's (parse kernel + checksum kernel), itself
+    pinned to the oracle above; the grid leaves between most flushes with idle_us = 40."""
+    import time
+    fs, arena, offs, flags = _batch()
+    lens = np.array([len(f["frame"]) for f in fs], np.uint32)
+    rng = np.random.default_rng(idle_us)
+    fl = np.array(flags, np.uint8)
+    fl[rng.random(len(fl)) < 0.05] = O.F_IP | O.F_L4P                 # refused where it cannot apply
+    a_svc, a_ref = arena.copy(), arena.copy()
+    c_svc = V.Context(0, max_arena=arena.nbytes, max_pkts=len(fs))
+    c_ref = V.Context(0, max_arena=arena.nbytes, max_pkts=len(fs))
+    c_svc.register(a_svc)
+    c_ref.register(a_ref)
+    c_svc.set_service(idle_us)
+    offs = np.array(offs, np.uint64)
+    iters = 40
+    for it in range(iters):
+        b = int(rng.choice([1, 2, 3, 4, 17, 64, 220]))
+        idx = rng.choice(len(fs), b, replace=False) if b < len(fs) else np.arange(len(fs))
+        o, L, f = offs[idx], lens[idx], fl[idx]
+        out_s, st_s = c_svc.egress_frames(a_svc, o, L, f)
+        out_r, st_r = c_ref.egress_frames(a_ref, o, L, f)
+        assert np.array_equal(st_s, st_r), it
+        assert np.array_equal(out_s, out_r), it
+        assert np.array_equal(a_svc, a_ref), it
+        t_end = time.perf_counter() + float(rng.integers(0, 3 * idle_us)) * 1e-6
+        while time.perf_counter() < t_end:
+            pass
+    assert c_svc.stats()["service_batches"] == iters and c_ref.stats()["service_batches"] == 0
+    c_svc.close()
+    c_ref.close()
 
 
 def test_egress_descriptor_random_frames():

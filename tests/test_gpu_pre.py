@@ -353,6 +353,58 @@ def test_ctx_submit_pre(V, orc, registered):
     ctx.close()
 
 
+@pytest.mark.parametrize("idle_us", [5000, 40])
+def test_service_submit_pre(V, orc, idle_us):
+    """Small zero-copy flushes of NAT'd frames through the service grid (vpcsum_ctx_submit_pre with
+    vpcsum_ctx_set_service: kernels.hip svc_pre_packet, one wave per frame), consecutive batches of
+    1..512 frames mixing F_PRE frames (48-B and 16-B pre-images, UDP stored 0), full-recompute
+    frames and refused descriptors, in WRITE and COMPUTE mode: the umem equals Java's bytes.  With
+    idle_us = 40 the grid leaves between most flushes and is relaunched (a batch it left unfinished
+    is re-run from the stored sums the host captured, never from the fields already rewritten)."""
+    import time
+    rng = np.random.default_rng(50 + idle_us)
+    after, desc, pre, want, wst = nat_case(orc, rng, 1500, O.SYNTH_FUZZ, pad=14)
+    full = rng.random(len(desc)) < 0.3
+    desc["flags"][full] &= 0xFF ^ O.F_PRE
+    desc["l3_ver"][7::101] = 5                               # refused by both paths
+    live = (desc["l3_ver"] != 5) & (desc["flags"] != 0)
+    d4 = desc.copy()                                         # 16-B entries: IPv4 only
+    d4["flags"][d4["l3_ver"] == 6] &= 0xFF ^ O.F_PRE
+    p4 = nat4_of(pre)
+    exp48, exp4 = expected_out(orc, want, desc), expected_out(orc, want, d4)
+    arena = np.concatenate([after, np.zeros(4096, np.uint8)])
+    base = arena.copy()
+    ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=len(desc))
+    ctx.register(arena)
+    ctx.set_service(idle_us)
+    iters = 60
+    for it in range(iters):
+        b = int(rng.choice([1, 2, 3, 4, 5, 32, 128, 512]))
+        lo = int(rng.integers(0, len(desc) - b + 1))
+        sl = slice(lo, lo + b)
+        fmt48 = it % 2 == 0
+        dd, pp, exp = (desc, pre, exp48) if fmt48 else (d4, p4, exp4)
+        mode = O.MODE_WRITE if it % 3 else O.MODE_COMPUTE
+        arena[:] = base
+        out = np.zeros(b, np.uint32)
+        st = np.zeros(b, np.uint8)
+        ctx.wait(ctx.submit_pre(arena, np.ascontiguousarray(dd[sl]), np.ascontiguousarray(pp[sl]), out, st, mode))
+        lv = live[sl]
+        what = f"it {it} n {b} fmt48 {fmt48} mode {mode}"
+        assert np.all(st[lv] == O.S_DONE) and np.all(st[desc["l3_ver"][sl] == 5] == O.S_BAD_DESC), what
+        assert np.array_equal(out[lv], exp[sl][lv]), what
+        if mode == O.MODE_WRITE:
+            assert_frames(arena[:len(want)], want, dd[sl][lv], what, whole=False)
+        else:
+            assert np.array_equal(arena, base), what
+        t_end = time.perf_counter() + float(rng.integers(0, 3 * idle_us)) * 1e-6
+        while time.perf_counter() < t_end:
+            pass
+    s = ctx.stats()
+    assert s["service_batches"] == iters and s["service_launches"] >= 1
+    ctx.close()
+
+
 def test_group_and_default_group_submit_pre(V, orc):
     """vpcsum_group_submit_pre over two contexts on one card, and vpcsum_batch_submit_pre on the
     process-wide group: the same bytes as Java."""

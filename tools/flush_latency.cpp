@@ -44,6 +44,19 @@ int main(int argc, char** argv) {
         desc[i].flags = VPCSUM_F_IP | VPCSUM_F_L4;
     }
     std::vector<uint32_t> out(nmax);
+    // NAT'd frames flushed from their pre-images (vpcsum_ctx_submit_pre, 16-B entries naming the
+    // addresses and ports): the same frames, every descriptor F_PRE
+    std::vector<vpcsum_desc_t> pdesc(desc);
+    std::vector<vpcsum_pre4_t> pre(nmax);
+    for (uint32_t i = 0; i < nmax; ++i) {
+        pdesc[i].flags |= VPCSUM_F_PRE;
+        const uint8_t* l3 = arena.data() + (size_t)i * stride;
+        memcpy(pre[i].src, l3 + 12, 4);
+        memcpy(pre[i].dst, l3 + 16, 4);
+        memcpy(pre[i].sport, l3 + 20, 2);
+        memcpy(pre[i].dport, l3 + 22, 2);
+        pre[i].mask = VPCSUM_NAT_SRC | VPCSUM_NAT_DST | VPCSUM_NAT_SPORT | VPCSUM_NAT_DPORT;
+    }
     // the same frames behind a 14-B Ethernet header, for the egress path that parses raw frames on
     // the GPU (vpcsum_ctx_egress_frames: offsets, lengths and per-frame flags only)
     std::vector<uint8_t> eth((size_t)nmax * stride + 4096, 0);
@@ -69,9 +82,12 @@ int main(int argc, char** argv) {
     // (re-loads) instead of predicated; 4 = release semantics on the completion count and `done`.  The configurations run interleaved in kRounds rounds of
     // iters / kRounds flushes per size, so that drift on the box hits all of them alike.
     // 5 = raw frames parsed on the GPU, two launches per flush (vpcsum_ctx_egress_frames).
-    constexpr int kCfg = 6;
+    // 6 / 7 = NAT'd frames from their pre-images (vpcsum_ctx_submit_pre), launched / service grid.
+    // 8 = raw frames through the service grid (parse + sum per frame, no launch).
+    constexpr int kCfg = 9;
     static const char* names[kCfg] = {"launch", "service", "service_no_inline", "service_clamped_loads",
-                                      "service_release_done", "egress_frames"};
+                                      "service_release_done", "egress_frames", "pre_launch", "pre_service",
+                                      "egress_frames_service"};
     static const uint32_t sizes[7] = {1u, 3u, 4u, 32u, 128u, 1024u, 8192u};
     constexpr int kRounds = 5;
     std::vector<double> us[kCfg][7];
@@ -80,7 +96,7 @@ int main(int argc, char** argv) {
             setenv("VPCSUM_SVC_INLINE", svc == 2 ? "0" : "1", 1);
             setenv("VPCSUM_SVC_CLAMP", svc == 3 ? "1" : "0", 1);
             setenv("VPCSUM_SVC_RELEASE_DONE", svc == 4 ? "1" : "0", 1);
-            if (vpcsum_ctx_set_service(ctx, (svc && svc < 5) ? 200000 : 0)) {
+            if (vpcsum_ctx_set_service(ctx, ((svc && svc < 5) || svc == 7 || svc == 8) ? 200000 : 0)) {
                 fprintf(stderr, "service: %s\n", vpcsum_last_error());
                 return 1;
             }
@@ -90,9 +106,11 @@ int main(int argc, char** argv) {
                 for (int it = 0; it < iters / kRounds + 20; ++it) {
                     uint64_t t = 0;
                     const auto t0 = std::chrono::steady_clock::now();
-                    const int rc = svc == 5
+                    const int rc = (svc == 5 || svc == 8)
                         ? vpcsum_ctx_egress_frames(ctx, eth.data(), eth.size(), foff.data(), flen.data(), fflags.data(),
                                                    b, out.data(), fst.data(), &t)
+                        : svc >= 6 ? vpcsum_ctx_submit_pre(ctx, arena.data(), arena.size(), pdesc.data(), pre.data(),
+                                                           VPCSUM_PRE_FMT_PRE4, b, out.data(), nullptr, VPCSUM_MODE_WRITE, &t)
                         : vpcsum_ctx_submit(ctx, arena.data(), arena.size(), desc.data(), b, out.data(), nullptr,
                                             VPCSUM_MODE_WRITE, &t);
                     if (rc || vpcsum_ctx_wait(ctx, t)) {

@@ -11,7 +11,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libvpcsum.so")
 SOURCES = ["kernels.hip", "nat.hip", "api.cpp"]
-HEADERS = ["internal.h", "device_common.h", os.path.join("..", "..", "include", "vpcsum.h")]
+HEADERS = ["internal.h", "device_common.h", "pre_common.h", os.path.join("..", "..", "include", "vpcsum.h")]
 ARCH = os.environ.get("VPCSUM_ARCH", "gfx950")
 
 

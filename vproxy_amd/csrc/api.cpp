@@ -153,10 +153,10 @@ struct Registered {
 
 // Zero-copy batches (frames read over PCIe) of at most this many packets run one wave per packet.
 constexpr uint32_t kZeroCopyWaveTeams = 4096;
-// Largest batch handed to the low-latency service (128 waves, one packet each per round); larger
-// ones are launched with a grid of their size, which is faster from ~1000 packets on
-// (tools/flush_latency.cpp: 1024 packets 48 us launched vs 57 us through the service).
-constexpr uint32_t kSvcBatchMax = 512;
+// kSvcBatchMax (internal.h): the largest batch handed to the low-latency service (128 waves, one
+// packet each per round); larger ones are launched with a grid of their size, which is faster from
+// ~1000 packets on (tools/flush_latency.cpp: 1024 packets 55 us launched vs 58 us through the
+// service, profiles/r05m_flush_latency.json).
 
 // Low-latency service of a context (kernels.hip k_csum_service).
 struct Service {
@@ -173,6 +173,8 @@ struct Service {
     vpcsum_desc_t* dh_desc = nullptr;
     uint32_t* dh_out = nullptr;
     uint8_t* dh_status = nullptr;
+    void* h_pre = nullptr;               // pre-images of a batch with F_PRE frames (kSvcBatchMax x 48 B)
+    void* dh_pre = nullptr;
     uint64_t par[3] = {0, 0, 0};         // arena, arena_len, arena_w last published
     bool par_valid = false;
     uint32_t posted = 0;                 // last batch published (seq)
@@ -482,6 +484,7 @@ static void svc_free(vpcsum_ctx* c) {
     if (v.h_desc) (void)hipHostFree(v.h_desc);
     if (v.h_out) (void)hipHostFree(v.h_out);
     if (v.h_status) (void)hipHostFree(v.h_status);
+    if (v.h_pre) (void)hipHostFree(v.h_pre);
     c->svc = Service();
 }
 
@@ -494,7 +497,6 @@ int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
             if (s.busy && slot_finish(c, s) != 0) return -1;
         svc_free(c);
         if (idle_us == 0) return 0;
-        if (c->max_pkts > kSvcMaxPkts) return fail("vpcsum_ctx_set_service: capacity %u > %u packets", c->max_pkts, kSvcMaxPkts);
         Service& v = c->svc;
         const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
         hipError_t e = hipSuccess;
@@ -503,6 +505,9 @@ int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
             (e = hipHostMalloc((void**)&v.h_desc, (size_t)c->max_pkts * sizeof(vpcsum_desc_t), fl)) != hipSuccess ||
             (e = hipHostMalloc((void**)&v.h_out, (size_t)c->max_pkts * 4, fl)) != hipSuccess ||
             (e = hipHostMalloc((void**)&v.h_status, (size_t)c->max_pkts, fl)) != hipSuccess ||
+            (e = hipHostMalloc((void**)&v.h_pre, (size_t)std::min(c->max_pkts, kSvcBatchMax) * sizeof(vpcsum_pre_t), fl)) !=
+                hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&v.dh_pre, v.h_pre, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&v.dh_desc, v.h_desc, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&v.dh_out, v.h_out, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&v.dh_status, v.h_status, 0)) != hipSuccess ||
@@ -515,6 +520,7 @@ int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
         v.mb->desc = (uint64_t)(uintptr_t)v.dh_desc;
         v.mb->out = (uint64_t)(uintptr_t)v.dh_out;
         v.mb->status = (uint64_t)(uintptr_t)v.dh_status;
+        v.mb->pre = (uint64_t)(uintptr_t)v.dh_pre;
         v.idle_ticks = (uint64_t)idle_us * 100u;   // s_memrealtime runs at 100 MHz
         const char* inl = getenv("VPCSUM_SVC_INLINE");
         v.inline_desc = !(inl && inl[0] == '0');
@@ -801,6 +807,92 @@ static int slot_rw_alloc(vpcsum_ctx* c, Slot& s, const char* what) {
 
 static int l4_field_host(int proto) { return proto == 6 ? 16 : proto == 17 ? 6 : (proto == 1 || proto == 58) ? 2 : -1; }
 
+// The service runs one batch at a time: the previous one done, its results handed over, before its
+// buffers are refilled.
+static int svc_drain(vpcsum_ctx* c) {
+    for (auto& o : c->slots)
+        if (o.busy && o.svc_seq && slot_finish(c, o) != 0) return -1;
+    return 0;
+}
+
+// Hand a zero-copy batch to the low-latency service (c->svc.on, n <= kSvcBatchMax): one batch at
+// a time; descriptors (and pre-images) into the service's buffers, the parameter block if it
+// changed, then the command word.  `base` is the device address of h_arena[0].  Caller holds c->mu
+// on c's device; slot s (ticket t) is free.
+// frames: h_desc is the service's own buffer, filled with SvcFrameRec records (egress frames).
+static int svc_post(vpcsum_ctx* c, Slot& s, uint64_t t, uint8_t* h_arena, uint64_t arena_len, uint8_t* base,
+                    const vpcsum_desc_t* h_desc, uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode,
+                    const void* h_pre, uint32_t pre_fmt, uint64_t* ticket, bool frames = false) {
+    Service& v = c->svc;
+    SvcMailbox* mb = v.mb;
+    if (!frames) memcpy(v.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
+    uint64_t cmd = frames ? kSvcFrames : 0;
+    if (h_pre) {
+        // the pre-images, each F_PRE frame's stored L4 sum copied into its entry's spare bytes
+        // (vpcsum_pre4_t rsv[1..2], vpcsum_pre_t rsv[0..1]): the kernel takes the sum from there,
+        // so a batch re-run by a fresh grid (svc_wait) computes from the same input
+        const size_t esz = pre_fmt == VPCSUM_PRE_FMT_PRE ? sizeof(vpcsum_pre_t) : sizeof(vpcsum_pre4_t);
+        const size_t at = pre_fmt == VPCSUM_PRE_FMT_PRE ? offsetof(vpcsum_pre_t, rsv) : offsetof(vpcsum_pre4_t, rsv) + 1;
+        memcpy(v.h_pre, h_pre, (size_t)n * esz);
+        for (uint32_t i = 0; i < n; ++i) {
+            const vpcsum_desc_t& d = h_desc[i];
+            const int fld = l4_field_host(d.l4_proto);
+            if (!(d.flags & VPCSUM_F_PRE) || fld < 0 || d.l3_off > arena_len || d.l3_len > arena_len - d.l3_off ||
+                (uint32_t)d.l4_off + fld + 2u > d.l3_len)
+                continue;   // no L4 sum to update, or refused by the kernel
+            memcpy((uint8_t*)v.h_pre + (size_t)i * esz + at, h_arena + d.l3_off + d.l4_off + fld, 2);
+        }
+        cmd |= kSvcPre | (pre_fmt == VPCSUM_PRE_FMT_PRE ? kSvcPreFmt : 0);
+    }
+    const uint64_t par[3] = {(uint64_t)(uintptr_t)base, arena_len, (mode & VPCSUM_MODE_WRITE) ? (uint64_t)(uintptr_t)base : 0};
+    if (!v.par_valid || memcmp(par, v.par, sizeof(par)) != 0) {
+        mb->arena = par[0];
+        mb->arena_len = par[1];
+        mb->arena_w = par[2];
+        memcpy(v.par, par, sizeof(par));
+        v.par_valid = true;
+        cmd |= kSvcParams;
+    }
+    const uint32_t seq = v.posted + 1 ? v.posted + 1 : 1;
+    // the first descriptors ride in the command's line, tagged with the batch.  All of them are
+    // rewritten for every batch, so a stale one always carries the previous batch's tag; the high
+    // word (with the tag) is stored after the low one.
+    for (int k = 0; k < kSvcInlineDesc; ++k) {
+        vpcsum_desc_t d;
+        if ((uint32_t)k < n) memcpy(&d, &h_desc[k], sizeof(d));
+        else memset(&d, 0, sizeof(d));
+        d.rsv = (uint8_t)seq;
+        uint64_t w[2];
+        memcpy(w, &d, sizeof(w));
+        uint64_t* dst = reinterpret_cast<uint64_t*>(&mb->idesc[k]);
+        __atomic_store_n(&dst[0], w[0], __ATOMIC_RELAXED);
+        __atomic_store_n(&dst[1], w[1], __ATOMIC_RELEASE);
+    }
+    cmd |= seq | ((uint64_t)n << 32) | ((mode & VPCSUM_MODE_VERIFY) ? kSvcVerify : 0) |
+           (v.inline_desc && n <= (uint32_t)kSvcInlineDesc ? kSvcInline : 0);
+#ifdef VPCSUM_SVC_STAMPS
+    v.t_post = std::chrono::steady_clock::now();
+    v.t_n = n;
+#endif
+    __atomic_store_n(&mb->cmd, cmd, __ATOMIC_RELEASE);
+    v.posted = seq;
+    ++c->svc_batches;
+    if (hipStreamQuery(v.stream) == hipSuccess && svc_launch(c, seq - 1) != 0) return -1;
+    s.zero_copy = true;
+    s.svc_seq = seq;
+    s.kind = 0;
+    s.busy = true;
+    s.ticket = t;
+    s.n = n;
+    s.mode = mode;
+    s.user_arena = h_arena;
+    s.user_desc = h_desc;
+    s.user_out = h_out;
+    s.user_status = h_status;
+    *ticket = t;
+    return 0;
+}
+
 int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, uint32_t n,
                       uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket) {
     try {
@@ -835,63 +927,9 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
             // results to pinned staging, and with MODE_WRITE stores the checksum fields straight
             // into the frames -- no DMA copy in either direction.
             uint8_t* base = dev_arena - lo;   // device address of h_arena[0]
-            Service& v = c->svc;
-            if (v.on && n <= kSvcBatchMax) {
-                // low-latency service: one batch at a time; descriptors into the service's buffer,
-                // the parameter block if it changed, then the command word
-                for (auto& o : c->slots)   // the previous service batch: done, results handed over
-                    if (o.busy && o.svc_seq && slot_finish(c, o) != 0) return -1;
-                SvcMailbox* mb = v.mb;
-                memcpy(v.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
-                const uint64_t par[3] = {(uint64_t)(uintptr_t)base, arena_len,
-                                         (mode & VPCSUM_MODE_WRITE) ? (uint64_t)(uintptr_t)base : 0};
-                uint64_t cmd = 0;
-                if (!v.par_valid || memcmp(par, v.par, sizeof(par)) != 0) {
-                    mb->arena = par[0];
-                    mb->arena_len = par[1];
-                    mb->arena_w = par[2];
-                    memcpy(v.par, par, sizeof(par));
-                    v.par_valid = true;
-                    cmd |= kSvcParams;
-                }
-                const uint32_t seq = v.posted + 1 ? v.posted + 1 : 1;
-                // the first descriptors ride in the command's line, tagged with the batch.  All of
-                // them are rewritten for every batch, so a stale one always carries the previous
-                // batch's tag; the high word (with the tag) is stored after the low one.
-                for (int k = 0; k < kSvcInlineDesc; ++k) {
-                    vpcsum_desc_t d;
-                    if ((uint32_t)k < n) memcpy(&d, &h_desc[k], sizeof(d));
-                    else memset(&d, 0, sizeof(d));
-                    d.rsv = (uint8_t)seq;
-                    uint64_t w[2];
-                    memcpy(w, &d, sizeof(w));
-                    uint64_t* dst = reinterpret_cast<uint64_t*>(&mb->idesc[k]);
-                    __atomic_store_n(&dst[0], w[0], __ATOMIC_RELAXED);
-                    __atomic_store_n(&dst[1], w[1], __ATOMIC_RELEASE);
-                }
-                cmd |= seq | ((uint64_t)n << 32) | ((mode & VPCSUM_MODE_VERIFY) ? kSvcVerify : 0) |
-                       (v.inline_desc && n <= (uint32_t)kSvcInlineDesc ? kSvcInline : 0);
-    #ifdef VPCSUM_SVC_STAMPS
-                v.t_post = std::chrono::steady_clock::now();
-                v.t_n = n;
-    #endif
-                __atomic_store_n(&mb->cmd, cmd, __ATOMIC_RELEASE);
-                v.posted = seq;
-                ++c->svc_batches;
-                if (hipStreamQuery(v.stream) == hipSuccess && svc_launch(c, seq - 1) != 0) return -1;
-                s.zero_copy = true;
-                s.svc_seq = seq;
-                s.kind = 0;
-                s.busy = true;
-                s.ticket = t;
-                s.n = n;
-                s.mode = mode;
-                s.user_arena = h_arena;
-                s.user_desc = h_desc;
-                s.user_out = h_out;
-                s.user_status = h_status;
-                *ticket = t;
-                return 0;
+            if (c->svc.on && n <= kSvcBatchMax) {
+                if (svc_drain(c) != 0) return -1;
+                return svc_post(c, s, t, h_arena, arena_len, base, h_desc, n, h_out, h_status, mode, nullptr, 0, ticket);
             }
             memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
             // up to kZeroCopyWaveTeams packets: one wave per packet (variant 12, 64 lanes x 4
@@ -986,8 +1024,6 @@ int vpcsum_ctx_submit_pre(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len,
         const uint64_t t = c->next_ticket++;
         Slot& s = c->slots[t & 1];
         if (s.busy && slot_finish(c, s) != 0) return -1;
-        if (slot_rw_alloc(c, s, "vpcsum_ctx_submit_pre allocation") != 0) return -1;
-        memcpy(s.h_rw, h_pre, (size_t)n * esz);
         uint64_t lo = UINT64_MAX, hi = 0;
         for (uint32_t i = 0; i < n; ++i) {
             const vpcsum_desc_t& d = h_desc[i];
@@ -999,6 +1035,15 @@ int vpcsum_ctx_submit_pre(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len,
         lo &= ~(uint64_t)15;
         uint8_t* dev_arena = hi > lo ? mapped_dev(c, h_arena + lo, hi - lo) : nullptr;
         const uint32_t wr = mode & VPCSUM_MODE_WRITE;
+        // a small flush from the registered umem: the service grid, F_PRE frames and the others in
+        // one batch (kernels.hip svc_pre_packet)
+        if (dev_arena && c->svc.on && n <= kSvcBatchMax) {
+            if (svc_drain(c) != 0) return -1;
+            return svc_post(c, s, t, h_arena, arena_len, dev_arena - lo, h_desc, n, h_out, h_status, mode, h_pre, pre_fmt,
+                            ticket);
+        }
+        if (slot_rw_alloc(c, s, "vpcsum_ctx_submit_pre allocation") != 0) return -1;
+        memcpy(s.h_rw, h_pre, (size_t)n * esz);
         if (dev_arena) {
             // registered arena (umem): in place; an F_PRE packet's header is all that crosses PCIe
             uint8_t* base = dev_arena - lo;
@@ -1141,6 +1186,25 @@ int vpcsum_ctx_egress_frames(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_l
         const uint64_t t = c->next_ticket++;
         Slot& s = c->slots[t & 1];
         if (s.busy && slot_finish(c, s) != 0) return -1;
+        if (n && c->svc.on && n <= kSvcBatchMax) {
+            // a small flush: the service grid parses and sums each frame (kernels.hip svc_frame_packet)
+            if (svc_drain(c) != 0) return -1;
+            SvcFrameRec* r = reinterpret_cast<SvcFrameRec*>(c->svc.h_desc);
+            for (uint32_t i = 0; i < n; ++i) {
+                SvcFrameRec x;
+                memset(&x, 0, sizeof(x));
+                x.off = h_frame_off[i];
+                x.len = h_frame_len[i];
+                x.flags = h_frame_flags[i];
+                memcpy(&r[i], &x, sizeof(x));
+            }
+            if (svc_post(c, s, t, h_arena, arena_len, base, c->svc.h_desc, n, h_out, h_status, VPCSUM_MODE_WRITE, nullptr, 0,
+                         ticket, true) != 0)
+                return -1;
+            s.user_arena = nullptr;   // written in place through the mapping
+            s.user_desc = nullptr;
+            return 0;
+        }
         if (n) {
             // the frames' own flags ride in the status staging: the parse reads them before the
             // checksum kernel, later on the same stream, overwrites them with the statuses

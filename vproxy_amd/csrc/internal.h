@@ -23,11 +23,13 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
 // no separate descriptor read over PCIe.
 constexpr int kSvcInlineDesc = 3;
 struct alignas(64) SvcMailbox {
-    uint64_t cmd;        // host: seq (bits 0..31, 0 = none yet) | n (32..59) | kSvcInline | kSvcStop | kSvcVerify | kSvcParams
+    uint64_t cmd;        // host: seq (bits 0..31, 0 = none yet) | n (32..55) | kSvcFrames | kSvcPre | kSvcPreFmt | kSvcInline |
+                         // kSvcStop | kSvcVerify | kSvcParams
     uint64_t rsv0;
     vpcsum_desc_t idesc[kSvcInlineDesc];   // host: descriptors 0..2 of the batch, rsv = (uint8_t)seq
     alignas(64) uint64_t arena;   // line 1, device addresses, read when kSvcParams: arena, then
-    uint64_t arena_len, arena_w, desc, out, status, opts, rsv;   // opts: kSvcOpt* (tooling)
+    uint64_t arena_len, arena_w, desc, out, status, opts, pre;   // opts: kSvcOpt* (tooling); pre: the
+                                                                 // service's pre-image buffer (kSvcPre batches)
     alignas(64) uint32_t done;   // device: last completed batch
     uint32_t pad_;
     uint64_t stamp[7];           // VPCSUM_SVC_STAMPS builds only: s_memrealtime per batch step
@@ -37,7 +39,22 @@ static_assert(offsetof(SvcMailbox, arena) == 64 && offsetof(SvcMailbox, done) ==
 constexpr uint64_t kSvcInline = 1ull << 60, kSvcStop = 1ull << 61, kSvcVerify = 1ull << 62, kSvcParams = 1ull << 63;
 constexpr uint64_t kSvcOptClampLoads = 1;   // A/B: the frame loads of a batch clamp instead of predicate
 constexpr uint64_t kSvcOptReleaseDone = 2;  // A/B: release semantics on the completion count and `done`
-constexpr uint32_t kSvcMaxPkts = (1u << 28) - 1;
+// a batch with VPCSUM_F_PRE frames: their pre-images are in the buffer `pre` names, 16-B
+// vpcsum_pre4_t entries, or 48-B vpcsum_pre_t ones with kSvcPreFmt
+constexpr uint64_t kSvcPre = 1ull << 58, kSvcPreFmt = 1ull << 59;
+// a batch of raw egress frames (vpcsum_ctx_egress_frames): the descriptor buffer (and the inline
+// descriptors) hold SvcFrameRec records, each frame is parsed on the GPU before it is summed
+constexpr uint64_t kSvcFrames = 1ull << 57;
+struct SvcFrameRec {
+    uint64_t off;    // the frame's offset in the arena
+    uint32_t len;    // its length
+    uint8_t flags;   // the VPCSUM_F_* sums it needs
+    uint8_t pad[2];
+    uint8_t tag;     // the inline records' batch tag (vpcsum_desc_t's rsv byte)
+};
+static_assert(sizeof(SvcFrameRec) == sizeof(vpcsum_desc_t), "a frame record takes a descriptor's slot");
+constexpr uint32_t kSvcMaxPkts = (1u << 24) - 1;   // the command's n field
+constexpr uint32_t kSvcBatchMax = 512;              // largest batch the host hands to the service (api.cpp)
 constexpr int kServiceGrid = 32;   // workgroups: 4 waves each, one packet per wave and round
 hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream);
 

@@ -21,6 +21,7 @@
 #include "vpcsum.h"
 #include "internal.h"
 #include "device_common.h"
+#include "pre_common.h"
 
 namespace vpcsum {
 
@@ -257,17 +258,143 @@ __device__ __forceinline__ void k1_packet(const uint8_t* __restrict__ arena, uin
     }
 }
 
+// A pre-image frame (VPCSUM_F_PRE) on the service grid, one wave per frame: k_pre's arithmetic
+// (nat.hip, pre_common.h:pre_sums) for the small zero-copy flushes of NAT'd frames.  The header
+// window (chunk k on lane k, predicated: only the chunks the frame needs cross PCIe) and the
+// pre-image (its 16-B pieces on lanes 32..34) come in one round trip and are staged in LDS; lane 0
+// rebuilds the IPv4 header sum, applies RFC 1624 eqn. 3 to the L4 sum and stores the two fields.
+// A UDP frame whose stored sum is 0 is summed in full by the whole wave (k1_packet without F_PRE),
+// where k_pre takes byte reads: the same value as Java's recompute.  The stored L4 sum comes from
+// the entry's spare bytes (vpcsum_pre4_t rsv[1..2], vpcsum_pre_t rsv[0..1]), where the host copied
+// it when it posted the batch: the frame's own field is what this flush overwrites, so a batch that
+// a leaving grid re-runs (api.cpp:svc_wait) must not read it back.
+constexpr int kSvcPreChunks = 24;   // 384 B: any IPv4 header, IPv6 with one extension header
+__device__ __forceinline__ uint4 shfl_u4(const uint4 v, int src) {
+    return make_uint4((uint32_t)__shfl((int)v.x, src, 64), (uint32_t)__shfl((int)v.y, src, 64),
+                      (uint32_t)__shfl((int)v.z, src, 64), (uint32_t)__shfl((int)v.w, src, 64));
+}
+
+template <bool PRED>
+__device__ __forceinline__ void svc_pre_packet(const uint8_t* __restrict__ arena, uint64_t arena_len, const uint4 dv,
+                                               const void* __restrict__ pre, int fmt, const uint32_t p,
+                                               uint32_t* __restrict__ out, uint8_t* __restrict__ status,
+                                               uint8_t* __restrict__ arena_w, const int tl) {
+    __shared__ uint4 s_pw[4][kSvcPreChunks];   // a window per wave of the 256-thread workgroup
+    if (!pre_desc_ok(dv, arena_len, fmt)) {
+        if (tl == 0) {
+            if (out) out[p] = 0;
+            if (status) status[p] = VPCSUM_S_BAD_DESC;
+        }
+        return;
+    }
+    const int wv = (threadIdx.x >> 6) & 3;
+    const uint64_t off = (uint64_t)dv.x | ((uint64_t)dv.y << 32);
+    const int l4o = dv.z >> 16;
+    const int ver = dv.w & 0xff, proto = (dv.w >> 8) & 0xff, fl = (dv.w >> 16) & 0xff;
+    const bool do_ip = (fl & VPCSUM_F_IP) != 0, do_l4 = (fl & VPCSUM_F_L4) != 0;
+    const int fld = l4_field(proto);
+    const uint8_t* l3 = arena + off;
+    const int r0 = (int)((uintptr_t)l3 & 15);
+    const int need = max(ver == 4 ? 20 : 40, do_l4 ? l4o + fld + 2 : l4o);
+    const int nch = (r0 + need + 15) >> 4;
+    const bool win = nch <= kSvcPreChunks;
+    const int npc = fmt ? 3 : 1;   // 16-B pieces of an entry
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (win && tl < nch) v = ((const uint4*)(l3 - r0))[tl];
+    else if (tl >= 32 && tl < 32 + npc) v = ((const uint4*)pre)[(size_t)p * npc + (tl - 32)];
+    if (tl < kSvcPreChunks) s_pw[wv][tl] = v;
+    const uint4 e0 = shfl_u4(v, 32), e1 = shfl_u4(v, 33), e2 = shfl_u4(v, 34);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    PreSums s = {0u, 0u, false};
+    if (tl == 0) {
+        const NatRw r = fmt ? nat_rw6(e0, e1, e2) : nat_rw4(e0);
+        const uint32_t sp = fmt ? e2.y : e0.w;   // the captured sum, big endian, in its top 16 bits
+        const int hc = (int)(((sp >> 8) & 0xff00u) | (sp >> 24));
+        s = win ? pre_sums((const uint8_t*)&s_pw[wv][0] + r0, ver, proto, l4o, do_ip, do_l4, r, hc)
+                : pre_sums(l3, ver, proto, l4o, do_ip, do_l4, r, hc);   // a window past 384 B: byte reads
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");   // s_pw is the next frame's
+    if (__shfl((int)s.udp_full, 0, 64)) {   // UDP stored 0: Java's recompute over the segment
+        k1_packet<64, 4, false, true, PRED>(arena, arena_len, dv, fl & ~VPCSUM_F_PRE, true, p, out, status, arena_w, tl);
+        return;
+    }
+    if (tl == 0) {
+        if (arena_w) {
+            uint8_t* w = arena_w + off;
+            if (do_ip) { w[10] = (uint8_t)(s.ipc >> 8); w[11] = (uint8_t)s.ipc; }
+            if (do_l4) { w[l4o + fld] = (uint8_t)(s.l4c >> 8); w[l4o + fld + 1] = (uint8_t)s.l4c; }
+        }
+        if (out) out[p] = (s.ipc & 0xffff) | ((s.l4c & 0xffff) << 16);
+        if (status) status[p] = VPCSUM_S_DONE;
+    }
+}
+
+__device__ __forceinline__ uint8_t parse_frame(const uint8_t* f, uint64_t o, uint32_t L, bool ok, uint8_t w, bool egress,
+                                               vpcsum_desc_t& d);
+
+// A raw egress frame on the service grid (vpcsum_ctx_egress_frames, one wave per frame): its first
+// 384 B (every byte parse_frame reads) come in one PCIe round trip and are staged in LDS; lane 0
+// parses them with the vswitch's rules (k_parse_ether's parse_frame, the frame's own flags) and the
+// wave sums the packet it found (k1_packet), where the launched path runs a parse kernel and a
+// checksum kernel.  rec: the frame's 16-B record {u64 offset; u32 length; u8 flags; ...}.
+constexpr int kSvcFrameChunks = 25;   // 384 B at any offset within a 16-B chunk
+template <bool PRED>
+__device__ __forceinline__ void svc_frame_packet(const uint8_t* __restrict__ arena, uint64_t arena_len, const uint4 rec,
+                                                 const uint32_t p, uint32_t* __restrict__ out,
+                                                 uint8_t* __restrict__ status, uint8_t* __restrict__ arena_w,
+                                                 const int tl) {
+    __shared__ uint4 s_fw[4][kSvcFrameChunks];
+    const int wv = (threadIdx.x >> 6) & 3;
+    const uint64_t o = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
+    const uint32_t L = rec.z;
+    const bool inb = o <= arena_len && (uint64_t)L <= arena_len - o;
+    const uint8_t* f = arena + o;
+    const int r0 = (int)((uintptr_t)f & 15);
+    const int nch = inb ? (r0 + (int)min(L, 384u) + 15) >> 4 : 0;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (tl < nch) v = ((const uint4*)(f - r0))[tl];
+    if (tl < kSvcFrameChunks) s_fw[wv][tl] = v;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    uint4 dd = make_uint4(0, 0, 0, 0);
+    uint32_t st = VPCSUM_S_BAD_DESC;
+    if (tl == 0) {
+        vpcsum_desc_t d;
+        st = parse_frame((const uint8_t*)&s_fw[wv][0] + r0, o, L, inb, (uint8_t)(rec.w & 0xffu), true, d);
+        dd = make_uint4((uint32_t)d.l3_off, (uint32_t)(d.l3_off >> 32), (uint32_t)d.l3_len | ((uint32_t)d.l4_off << 16),
+                        (uint32_t)d.l3_ver | ((uint32_t)d.l4_proto << 8) | ((uint32_t)d.flags << 16));
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");   // s_fw is the next frame's
+    dd = shfl_u4(dd, 0);
+    if (__shfl((int)st, 0, 64) != 0) {   // refused: nothing written, handed back by the caller
+        if (tl == 0) {
+            if (out) out[p] = 0;
+            if (status) status[p] = VPCSUM_S_BAD_DESC;
+        }
+        return;
+    }
+    k1_packet<64, 4, false, true, PRED>(arena, arena_len, dd, 0, false, p, out, status, arena_w, tl);
+}
+
 // Body for workgroup `blk` of a grid of `gdim` workgroups (k_csum: the launch grid;
 // k_csum_service: the persistent service grid, once per batch).
 // PRED: chunks past the packet end are not loaded (exec-masked) instead of re-loading the last
 // chunk.  On device memory the clamped re-load is a cache hit and keeps the loads branch-free;
 // on uncached host memory (zero-copy frames) every such load is another PCIe read.
-template <int TEAM, int U, bool VERIFY, bool NT, bool PRED = false>
+// SVC (the service grid, TEAM 64): 1 = F_PRE descriptors take svc_pre_packet with the pre-images
+// at `pre` (fmt 0: vpcsum_pre4_t, 1: vpcsum_pre_t; without `pre` they are no-ops, as everywhere
+// else); 2 = `desc` holds raw frame records (svc_frame_packet).
+template <int TEAM, int U, bool VERIFY, bool NT, bool PRED = false, int SVC = 0>
 __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                        const uint8_t* __restrict__ flags_override,
-                                       uint8_t* __restrict__ arena_w, uint32_t blk, uint32_t gdim) {
+                                       uint8_t* __restrict__ arena_w, uint32_t blk, uint32_t gdim,
+                                       const void* __restrict__ pre = nullptr, int pre_fmt = 0) {
+    static_assert(SVC == 0 || TEAM == 64, "the service grid's frames take a whole wave");
     const int tl = threadIdx.x & (TEAM - 1);
     const uint32_t team = (blk * 256u + threadIdx.x) / TEAM;
     const uint32_t nteams = gdim * (256u / TEAM);
@@ -286,8 +413,18 @@ __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64
             dnext = desc[p + nteams];
             if (flags_override) fnext = flags_override[p + nteams];
         }
-        k1_packet<TEAM, U, VERIFY, NT, PRED>(arena, arena_len, dv, fov, flags_override != nullptr, p, out, status,
-                                             arena_w, tl);
+        if constexpr (SVC == 2) {
+            svc_frame_packet<PRED>(arena, arena_len, dv, p, out, status, arena_w, tl);
+        } else {
+            if constexpr (SVC == 1) {
+                if (pre && (((dv.w >> 16) & 0xffu) & VPCSUM_F_PRE)) {
+                    svc_pre_packet<PRED>(arena, arena_len, dv, pre, pre_fmt, p, out, status, arena_w, tl);
+                    continue;
+                }
+            }
+            k1_packet<TEAM, U, VERIFY, NT, PRED>(arena, arena_len, dv, fov, flags_override != nullptr, p, out, status,
+                                                 arena_w, tl);
+        }
     }
 }
 
@@ -1212,8 +1349,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_pe
 __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* __restrict__ ctr, uint32_t seen,
                                                       uint64_t idle_ticks) {
     // batch parameters, read over PCIe by thread 0 when the host flags them as changed and kept
-    // in LDS across batches: arena, arena_len, arena_w, desc, out, status
-    __shared__ uint64_t s_par[7];
+    // in LDS across batches: arena, arena_len, arena_w, desc, out, status, opts, pre
+    __shared__ uint64_t s_par[8];
     __shared__ uint64_t s_cmd;
     __shared__ uint4 s_idesc[kSvcInlineDesc];   // workgroup 0: the inline descriptors of the batch
     __shared__ uint32_t s_inl;
@@ -1295,7 +1432,9 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                 s_par[3] = (uint64_t)q[1].z | ((uint64_t)q[1].w << 32);   // desc
                 s_par[4] = (uint64_t)q[2].x | ((uint64_t)q[2].y << 32);   // out
                 s_par[5] = (uint64_t)q[2].z | ((uint64_t)q[2].w << 32);   // status
-                s_par[6] = __builtin_nontemporal_load((const uint64_t*)&mb->opts);
+                const v4u q3 = __builtin_nontemporal_load(pb + 3);   // opts, pre (same line)
+                s_par[6] = (uint64_t)q3.x | ((uint64_t)q3.y << 32);
+                s_par[7] = (uint64_t)q3.z | ((uint64_t)q3.w << 32);
             }
             s_cmd = got;
 #ifdef VPCSUM_SVC_STAMPS
@@ -1314,6 +1453,8 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         uint8_t* status = (uint8_t*)s_par[5];
         const bool pred = (s_par[6] & kSvcOptClampLoads) == 0;
         const bool rel_done = (s_par[6] & kSvcOptReleaseDone) != 0;
+        const void* pre = (cmd & kSvcPre) ? (const void*)s_par[7] : nullptr;
+        const int pre_fmt = (cmd & kSvcPreFmt) ? 1 : 0;
         __syncthreads();   // s_cmd / s_par are rewritten next round
         if (cmd == 0) return;
         have_par = true;
@@ -1328,13 +1469,19 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         if (pred) {
             if (cmd & kSvcVerify)
                 k1_run<64, 4, true, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+            else if (cmd & kSvcFrames)
+                k1_run<64, 4, false, true, true, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
             else
-                k1_run<64, 4, false, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+                k1_run<64, 4, false, true, true, 1>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x,
+                                                    gridDim.x, pre, pre_fmt);
         } else {
             if (cmd & kSvcVerify)
                 k1_run<64, 4, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+            else if (cmd & kSvcFrames)
+                k1_run<64, 4, false, true, false, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
             else
-                k1_run<64, 4, false, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+                k1_run<64, 4, false, true, false, 1>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x,
+                                                     gridDim.x, pre, pre_fmt);
         }
         // the workgroup's stores are complete (barrier); thread 0 releases them system-wide and
         // counts the workgroup; the last participating workgroup publishes `done`
@@ -1627,6 +1774,80 @@ __device__ bool pe_ipv6_from(const uint8_t* b, uint32_t avail, uint32_t& total, 
     return pe_l4(false, 6, proto, b + l4o, seg);
 }
 
+// One frame at f (frame bytes: the arena, or a staged copy of at least its first 384 B -- no byte
+// past offset 381 is ever read: 18 B of Ethernet / 802.1Q, 40 + 8 + 255 of IPv6 and its extension
+// header, 60 of TCP header), o its arena offset, L its length, ok its bounds check: the descriptor
+// (flags from w: egress, every flag must be honoured; ingress, those the frame allows) and the
+// status byte (0 = parsed, S_BAD_DESC = refused).
+__device__ __forceinline__ uint8_t parse_frame(const uint8_t* f, uint64_t o, uint32_t L, bool ok, uint8_t w, bool egress,
+                                               vpcsum_desc_t& d) {
+    d.l3_off = 0; d.l3_len = 0; d.l4_off = 0; d.l3_ver = 0; d.l4_proto = 0; d.flags = 0; d.rsv = 0;
+    uint8_t st = VPCSUM_S_BAD_DESC;
+    ok = ok && L >= 14;
+    uint32_t hl = 14, typ = 0;
+    if (ok) {
+        typ = ld16(f + 12);
+        if (typ == 0x8100) {
+            if (L < 18) ok = false;
+            else { typ = ld16(f + 16); hl = 18; }
+        }
+    }
+    if (ok) {
+        const uint8_t* b = f + hl;
+        const uint32_t avail = L - hl;
+        if (typ == 0x0800 && avail >= 20) {
+            // Ipv4Packet.initPartial: the EtherType decided IPv4, the version nibble is not read
+            const uint32_t ihl = b[0] & 15u;
+            const uint32_t total = ld16(b + 2);
+            if (avail >= ihl * 4 && ihl >= 5 && total >= ihl * 4 && total <= avail &&
+                pe_l4(true, 4, b[9], b + ihl * 4, total - ihl * 4)) {
+                d.l3_off = o + hl; d.l3_len = (uint16_t)total; d.l4_off = (uint16_t)(ihl * 4);
+                d.l3_ver = 4; d.l4_proto = b[9];
+                st = 0;
+            }
+        } else if (typ == 0x86DD && avail >= 40) {
+            uint32_t total = 0;
+            int l4o = 40, proto = b[6];
+            bool good;
+            if (v6_needs_next(b[6])) {
+                good = pe_ipv6_from(b, avail, total, l4o, proto);   // initPartial defers to from()
+            } else {
+                const uint32_t pl = ld16(b + 4);
+                total = 40 + pl;
+                good = pl != 0 && total <= avail && pe_l4(true, 6, proto, b + 40, pl);
+            }
+            // l3_len is 16 bits: an IPv6 packet above 65535 B (payloadLength > 65495) cannot be
+            // described (it never fits a umem frame); refused
+            if (good && total <= 0xffff) {
+                d.l3_off = o + hl; d.l3_len = (uint16_t)total; d.l4_off = (uint16_t)l4o;
+                d.l3_ver = 6; d.l4_proto = (uint8_t)proto;
+                st = 0;
+            }
+        }
+    }
+    if (st == 0) {
+        // fwant (egress): the frame's own flags, all of which must be honoured -- a frame that
+        // cannot take one (an IPv4 header sum on IPv6, an L4 sum its segment does not hold, a
+        // pseudo-header sum for ICMPv4) is refused, so nothing is written and the caller hands
+        // it back.  want (ingress): the sums the frame allows, of those asked.
+        uint8_t fl = 0;
+        const bool ip_ok = d.l3_ver == 4;
+        const int fld = l4_field(d.l4_proto);
+        const bool l4_ok = fld >= 0 && !(d.l3_ver == 4 && d.l4_proto == 58) && d.l3_len - d.l4_off >= fld + 2;
+        if ((w & VPCSUM_F_IP) && ip_ok) fl |= VPCSUM_F_IP;
+        if ((w & VPCSUM_F_L4) && l4_ok) fl |= VPCSUM_F_L4;
+        else if ((w & VPCSUM_F_L4P) && l4_ok && d.l4_proto != 1) fl |= VPCSUM_F_L4P;
+        if (egress && (fl != (w & (VPCSUM_F_IP | VPCSUM_F_L4 | VPCSUM_F_L4P)) ||
+                      (w & ~(VPCSUM_F_IP | VPCSUM_F_L4 | VPCSUM_F_L4P)) || (fl & VPCSUM_F_L4 && fl & VPCSUM_F_L4P))) {
+            st = VPCSUM_S_BAD_DESC;
+            d.l3_off = 0; d.l3_len = 0; d.l4_off = 0; d.l3_ver = 0; d.l4_proto = 0;
+            fl = 0;
+        }
+        d.flags = fl;
+    }
+    return st;
+}
+
 __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                     const uint64_t* __restrict__ foff,
                                                     const uint32_t* __restrict__ flen, uint32_t n, uint8_t want,
@@ -1644,72 +1865,9 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
         const uint64_t o = act ? foff[p] : 0;
         const uint32_t L = act ? flen[p] : 0;
         vpcsum_desc_t d;
-        d.l3_off = 0; d.l3_len = 0; d.l4_off = 0; d.l3_ver = 0; d.l4_proto = 0; d.flags = 0; d.rsv = 0;
-        uint8_t st = VPCSUM_S_BAD_DESC;
-        bool ok = act && o <= arena_len && (uint64_t)L <= arena_len - o && L >= 14;
-        const uint8_t* f = arena + o;
-        uint32_t hl = 14, typ = 0;
-        if (ok) {
-            typ = ld16(f + 12);
-            if (typ == 0x8100) {
-                if (L < 18) ok = false;
-                else { typ = ld16(f + 16); hl = 18; }
-            }
-        }
-        if (ok) {
-            const uint8_t* b = f + hl;
-            const uint32_t avail = L - hl;
-            if (typ == 0x0800 && avail >= 20) {
-                // Ipv4Packet.initPartial: the EtherType decided IPv4, the version nibble is not read
-                const uint32_t ihl = b[0] & 15u;
-                const uint32_t total = ld16(b + 2);
-                if (avail >= ihl * 4 && ihl >= 5 && total >= ihl * 4 && total <= avail &&
-                    pe_l4(true, 4, b[9], b + ihl * 4, total - ihl * 4)) {
-                    d.l3_off = o + hl; d.l3_len = (uint16_t)total; d.l4_off = (uint16_t)(ihl * 4);
-                    d.l3_ver = 4; d.l4_proto = b[9];
-                    st = 0;
-                }
-            } else if (typ == 0x86DD && avail >= 40) {
-                uint32_t total = 0;
-                int l4o = 40, proto = b[6];
-                bool good;
-                if (v6_needs_next(b[6])) {
-                    good = pe_ipv6_from(b, avail, total, l4o, proto);   // initPartial defers to from()
-                } else {
-                    const uint32_t pl = ld16(b + 4);
-                    total = 40 + pl;
-                    good = pl != 0 && total <= avail && pe_l4(true, 6, proto, b + 40, pl);
-                }
-                // l3_len is 16 bits: an IPv6 packet above 65535 B (payloadLength > 65495) cannot be
-                // described (it never fits a umem frame); refused
-                if (good && total <= 0xffff) {
-                    d.l3_off = o + hl; d.l3_len = (uint16_t)total; d.l4_off = (uint16_t)l4o;
-                    d.l3_ver = 6; d.l4_proto = (uint8_t)proto;
-                    st = 0;
-                }
-            }
-        }
-        if (st == 0) {
-            // fwant (egress): the frame's own flags, all of which must be honoured -- a frame that
-            // cannot take one (an IPv4 header sum on IPv6, an L4 sum its segment does not hold, a
-            // pseudo-header sum for ICMPv4) is refused, so nothing is written and the caller hands
-            // it back.  want (ingress): the sums the frame allows, of those asked.
-            const uint8_t w = fwant ? fwant[p] : want;
-            uint8_t fl = 0;
-            const bool ip_ok = d.l3_ver == 4;
-            const int fld = l4_field(d.l4_proto);
-            const bool l4_ok = fld >= 0 && !(d.l3_ver == 4 && d.l4_proto == 58) && d.l3_len - d.l4_off >= fld + 2;
-            if ((w & VPCSUM_F_IP) && ip_ok) fl |= VPCSUM_F_IP;
-            if ((w & VPCSUM_F_L4) && l4_ok) fl |= VPCSUM_F_L4;
-            else if ((w & VPCSUM_F_L4P) && l4_ok && d.l4_proto != 1) fl |= VPCSUM_F_L4P;
-            if (fwant && (fl != (w & (VPCSUM_F_IP | VPCSUM_F_L4 | VPCSUM_F_L4P)) ||
-                          (w & ~(VPCSUM_F_IP | VPCSUM_F_L4 | VPCSUM_F_L4P)) || (fl & VPCSUM_F_L4 && fl & VPCSUM_F_L4P))) {
-                st = VPCSUM_S_BAD_DESC;
-                d.l3_off = 0; d.l3_len = 0; d.l4_off = 0; d.l3_ver = 0; d.l4_proto = 0;
-                fl = 0;
-            }
-            d.flags = fl;
-        }
+        const uint8_t w = act ? (fwant ? fwant[p] : want) : 0;
+        const uint8_t st = parse_frame(arena + o, o, L, act && o <= arena_len && (uint64_t)L <= arena_len - o, w,
+                                       fwant != nullptr, d);
         if (act) {
             desc[p] = d;
             if (status) status[p] = st;

@@ -265,13 +265,17 @@ class FrameEgressBatch:
     umem offset and length (chunk.getAddr() + pkb.pktOff, pkb.pktBuf.length(): padding included)
     and its F_* flags -- and ``complete_tx`` has the GPU parse the frames with the vswitch's rules and
     write their sums in place, in one submission.  A frame the GPU refuses (not parsable as IP, or
-    flags it cannot honour) is handed back untouched (``handed_back``)."""
+    flags it cannot honour) is handed back untouched (``handed_back``).  With ``service_idle_us`` > 0
+    flushes of up to 512 frames go to the low-latency service grid, which parses and sums each frame
+    in one pass (no kernel launch)."""
 
-    def __init__(self, arena: np.ndarray, capacity: int = 4096, device: int = 0):
+    def __init__(self, arena: np.ndarray, capacity: int = 4096, device: int = 0, service_idle_us: int = 0):
         self.arena = arena
         self.capacity = capacity
         self.ctx = V.Context(device, max_arena=max(arena.nbytes, 1 << 16), max_pkts=capacity)
         self.ctx.register(arena)
+        if service_idle_us:
+            self.ctx.set_service(service_idle_us)
         self.off = np.zeros(capacity, np.uint64)
         self.len = np.zeros(capacity, np.uint32)
         self.flags = np.zeros(capacity, np.uint8)
