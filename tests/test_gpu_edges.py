@@ -164,7 +164,8 @@ def test_edges_host_context(V, orc, packets, service):
         ctx.close()
 
 
-def test_edges_parsed_and_verified(V, orc, packets):
+@pytest.mark.parametrize("service", [False, True])
+def test_edges_parsed_and_verified(V, orc, packets, service):
     """Received frames (Ethernet + the edge packets) parsed and verified on the GPU in one
     submission: ICMPv4-in-IPv6 and extension-header frames get the reference's verdicts."""
     frames = E.ether_frames(packets)
@@ -178,7 +179,10 @@ def test_edges_parsed_and_verified(V, orc, packets):
     arena = np.frombuffer(bytes(arena) + bytes(4096), np.uint8).copy()
     ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=len(frames))
     ctx.register(arena)
+    if service:
+        ctx.set_service(20000)
     out, st = ctx.verify_frames(arena, np.array(offs), np.array(lens))
+    assert ctx.stats()["service_batches"] == (1 if service and len(frames) <= 512 else 0)
     ctx.close()
     for i, f in enumerate(frames):
         info, err = O.parse_ether(f)

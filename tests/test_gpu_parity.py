@@ -1112,6 +1112,20 @@ def test_verify_frames_rx_batch(V, orc):
         st3 = np.zeros(len(dd), np.uint8)
         ctx.wait(ctx.submit(a, dd, None, st3, O.MODE_VERIFY))
         assert np.array_equal(st3, want_st[ok])
+    # RX batches of up to 512 frames on the service grid (parse + verify per frame, no launch), with
+    # and without out words
+    ctx.set_service(20000)
+    offs_a, lens_a = np.array(offs), np.array(lens)
+    for lo in range(0, len(frames), 400):
+        sl = slice(lo, min(lo + 400, len(frames)))
+        out4, st4 = ctx.verify_frames(arena, offs_a[sl], lens_a[sl])
+        assert np.array_equal(st4, want_st[sl]), lo
+        ok4 = (want_st[sl] & O.S_BAD_DESC) == 0
+        assert np.array_equal(out4[ok4], want_out[sl][ok4]), lo
+        _, st5 = ctx.verify_frames(arena, offs_a[sl], lens_a[sl], sums=False)
+        assert np.array_equal(st5, want_st[sl]), lo
+    assert ctx.stats()["service_batches"] == 2 * ((len(frames) + 399) // 400)
+    assert np.array_equal(arena, before)
     ctx.close()
 
 
@@ -1299,7 +1313,8 @@ def test_windowed_k2_past_4gib(V, orc, order):
     torch.cuda.empty_cache()
 
 
-def test_parse_rules_on_gpu(V, orc):
+@pytest.mark.parametrize("service", [False, True])
+def test_parse_rules_on_gpu(V, orc, service):
     """k_parse_ether and ctx_verify_frames against the oracle's parse on frames at every edge of
     the reference's parse rules (tests/edgevec.py:parse_cases): TCP under 20 B, UDP under 8 B,
     empty ICMP, the version nibble not read by initPartial, the full Ipv6Packet.from behind an
@@ -1322,7 +1337,10 @@ def test_parse_rules_on_gpu(V, orc):
     got, stn = V.tensor_to_desc(d), st.cpu().numpy()
     ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=n)
     ctx.register(arena)
+    if service:   # the service grid parses each frame from its first 384 B staged in LDS
+        ctx.set_service(20000)
     vout, vst = ctx.verify_frames(arena, np.array(offs), np.array(lens))
+    assert ctx.stats()["service_batches"] == (1 if service else 0)
     ctx.close()
     for i, (f, ok, why) in enumerate(cases):
         info, err = O.parse_ether(f)

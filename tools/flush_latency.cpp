@@ -84,10 +84,12 @@ int main(int argc, char** argv) {
     // 5 = raw frames parsed on the GPU, two launches per flush (vpcsum_ctx_egress_frames).
     // 6 / 7 = NAT'd frames from their pre-images (vpcsum_ctx_submit_pre), launched / service grid.
     // 8 = raw frames through the service grid (parse + sum per frame, no launch).
-    constexpr int kCfg = 9;
+    // 9 / 10 = ingress verify of received frames, status bytes only (vpcsum_ctx_verify_frames, the
+    // GpuCsumBatch.verifyFrames form), launched (parse + verify kernels) / service grid.
+    constexpr int kCfg = 11;
     static const char* names[kCfg] = {"launch", "service", "service_no_inline", "service_clamped_loads",
                                       "service_release_done", "egress_frames", "pre_launch", "pre_service",
-                                      "egress_frames_service"};
+                                      "egress_frames_service", "verify_frames", "verify_frames_service"};
     static const uint32_t sizes[7] = {1u, 3u, 4u, 32u, 128u, 1024u, 8192u};
     constexpr int kRounds = 5;
     std::vector<double> us[kCfg][7];
@@ -96,7 +98,7 @@ int main(int argc, char** argv) {
             setenv("VPCSUM_SVC_INLINE", svc == 2 ? "0" : "1", 1);
             setenv("VPCSUM_SVC_CLAMP", svc == 3 ? "1" : "0", 1);
             setenv("VPCSUM_SVC_RELEASE_DONE", svc == 4 ? "1" : "0", 1);
-            if (vpcsum_ctx_set_service(ctx, ((svc && svc < 5) || svc == 7 || svc == 8) ? 200000 : 0)) {
+            if (vpcsum_ctx_set_service(ctx, ((svc && svc < 5) || svc == 7 || svc == 8 || svc == 10) ? 200000 : 0)) {
                 fprintf(stderr, "service: %s\n", vpcsum_last_error());
                 return 1;
             }
@@ -106,7 +108,10 @@ int main(int argc, char** argv) {
                 for (int it = 0; it < iters / kRounds + 20; ++it) {
                     uint64_t t = 0;
                     const auto t0 = std::chrono::steady_clock::now();
-                    const int rc = (svc == 5 || svc == 8)
+                    const int rc = svc >= 9
+                        ? vpcsum_ctx_verify_frames(ctx, eth.data(), eth.size(), foff.data(), flen.data(), b, nullptr,
+                                                   fst.data(), &t)
+                        : (svc == 5 || svc == 8)
                         ? vpcsum_ctx_egress_frames(ctx, eth.data(), eth.size(), foff.data(), flen.data(), fflags.data(),
                                                    b, out.data(), fst.data(), &t)
                         : svc >= 6 ? vpcsum_ctx_submit_pre(ctx, arena.data(), arena.size(), pdesc.data(), pre.data(),

@@ -1142,6 +1142,26 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
         const uint64_t t = c->next_ticket++;
         Slot& s = c->slots[t & 1];
         if (s.busy && slot_finish(c, s) != 0) return -1;
+        if (n && c->svc.on && n <= kSvcBatchMax) {
+            // a small received batch: the service grid parses and verifies each frame
+            // (kernels.hip svc_frame_packet), the sums into its own buffer (copied out only with h_out)
+            if (svc_drain(c) != 0) return -1;
+            SvcFrameRec* r = reinterpret_cast<SvcFrameRec*>(c->svc.h_desc);
+            for (uint32_t i = 0; i < n; ++i) {
+                SvcFrameRec x;
+                memset(&x, 0, sizeof(x));
+                x.off = h_frame_off[i];
+                x.len = h_frame_len[i];
+                x.flags = VPCSUM_F_IP | VPCSUM_F_L4;   // ingress: the sums each frame allows
+                memcpy(&r[i], &x, sizeof(x));
+            }
+            if (svc_post(c, s, t, const_cast<uint8_t*>(h_arena), arena_len, base, c->svc.h_desc, n, h_out, h_status,
+                         VPCSUM_MODE_VERIFY, nullptr, 0, ticket, true) != 0)
+                return -1;
+            s.user_arena = nullptr;
+            s.user_desc = nullptr;
+            return 0;
+        }
         if (n) {
             // parse the frames where they lie (zero-copy), then verify the descriptors it built
             memcpy(s.h_foff, h_frame_off, (size_t)n * 8);

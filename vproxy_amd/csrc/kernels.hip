@@ -334,13 +334,15 @@ __device__ __forceinline__ void svc_pre_packet(const uint8_t* __restrict__ arena
 __device__ __forceinline__ uint8_t parse_frame(const uint8_t* f, uint64_t o, uint32_t L, bool ok, uint8_t w, bool egress,
                                                vpcsum_desc_t& d);
 
-// A raw egress frame on the service grid (vpcsum_ctx_egress_frames, one wave per frame): its first
-// 384 B (every byte parse_frame reads) come in one PCIe round trip and are staged in LDS; lane 0
-// parses them with the vswitch's rules (k_parse_ether's parse_frame, the frame's own flags) and the
-// wave sums the packet it found (k1_packet), where the launched path runs a parse kernel and a
-// checksum kernel.  rec: the frame's 16-B record {u64 offset; u32 length; u8 flags; ...}.
+// A raw frame on the service grid, one wave per frame: an egress frame (vpcsum_ctx_egress_frames)
+// or, VERIFY, a received one (vpcsum_ctx_verify_frames).  Its first 384 B (every byte parse_frame
+// reads) come in one PCIe round trip and are staged in LDS; lane 0 parses them with the vswitch's
+// rules (k_parse_ether's parse_frame: egress, the frame's own flags, all honoured; ingress, those of
+// F_IP / F_L4 the frame allows) and the wave sums or verifies the packet it found (k1_packet),
+// where the launched path runs a parse kernel and a checksum kernel.  rec: the frame's 16-B record
+// {u64 offset; u32 length; u8 flags; ...}.
 constexpr int kSvcFrameChunks = 25;   // 384 B at any offset within a 16-B chunk
-template <bool PRED>
+template <bool VERIFY, bool PRED>
 __device__ __forceinline__ void svc_frame_packet(const uint8_t* __restrict__ arena, uint64_t arena_len, const uint4 rec,
                                                  const uint32_t p, uint32_t* __restrict__ out,
                                                  uint8_t* __restrict__ status, uint8_t* __restrict__ arena_w,
@@ -362,7 +364,7 @@ __device__ __forceinline__ void svc_frame_packet(const uint8_t* __restrict__ are
     uint32_t st = VPCSUM_S_BAD_DESC;
     if (tl == 0) {
         vpcsum_desc_t d;
-        st = parse_frame((const uint8_t*)&s_fw[wv][0] + r0, o, L, inb, (uint8_t)(rec.w & 0xffu), true, d);
+        st = parse_frame((const uint8_t*)&s_fw[wv][0] + r0, o, L, inb, (uint8_t)(rec.w & 0xffu), !VERIFY, d);
         dd = make_uint4((uint32_t)d.l3_off, (uint32_t)(d.l3_off >> 32), (uint32_t)d.l3_len | ((uint32_t)d.l4_off << 16),
                         (uint32_t)d.l3_ver | ((uint32_t)d.l4_proto << 8) | ((uint32_t)d.flags << 16));
     }
@@ -376,7 +378,7 @@ __device__ __forceinline__ void svc_frame_packet(const uint8_t* __restrict__ are
         }
         return;
     }
-    k1_packet<64, 4, false, true, PRED>(arena, arena_len, dd, 0, false, p, out, status, arena_w, tl);
+    k1_packet<64, 4, VERIFY, true, PRED>(arena, arena_len, dd, 0, false, p, out, status, arena_w, tl);
 }
 
 // Body for workgroup `blk` of a grid of `gdim` workgroups (k_csum: the launch grid;
@@ -414,7 +416,7 @@ __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64
             if (flags_override) fnext = flags_override[p + nteams];
         }
         if constexpr (SVC == 2) {
-            svc_frame_packet<PRED>(arena, arena_len, dv, p, out, status, arena_w, tl);
+            svc_frame_packet<VERIFY, PRED>(arena, arena_len, dv, p, out, status, arena_w, tl);
         } else {
             if constexpr (SVC == 1) {
                 if (pre && (((dv.w >> 16) & 0xffu) & VPCSUM_F_PRE)) {
@@ -1467,7 +1469,9 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         // bytes, results) instead of K2's per-unit iterations, which a latency of ~3 us per
         // round trip would serialize
         if (pred) {
-            if (cmd & kSvcVerify)
+            if ((cmd & kSvcVerify) && (cmd & kSvcFrames))
+                k1_run<64, 4, true, true, true, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+            else if (cmd & kSvcVerify)
                 k1_run<64, 4, true, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
             else if (cmd & kSvcFrames)
                 k1_run<64, 4, false, true, true, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
@@ -1475,7 +1479,9 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                 k1_run<64, 4, false, true, true, 1>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x,
                                                     gridDim.x, pre, pre_fmt);
         } else {
-            if (cmd & kSvcVerify)
+            if ((cmd & kSvcVerify) && (cmd & kSvcFrames))
+                k1_run<64, 4, true, true, false, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+            else if (cmd & kSvcVerify)
                 k1_run<64, 4, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
             else if (cmd & kSvcFrames)
                 k1_run<64, 4, false, true, false, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
