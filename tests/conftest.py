@@ -24,10 +24,14 @@ def orc():
 
 @pytest.fixture(autouse=True)
 def _sync_after_gpu_test(request):
-    """VPCSUM_SYNC_EACH_TEST=1 (debugging): synchronise the device after every GPU test, so that a
-    fault from asynchronous work (a service grid still polling, a kernel on another stream) is
-    reported against the test that started it, not the next one."""
+    """Every GPU test ends with a device synchronise (and a garbage collection first, so contexts
+    the test dropped are destroyed -- their service grids stopped -- inside it): a fault from
+    asynchronous work (a service grid still polling, a kernel on another stream) is reported against
+    the test that started it, not a later one.  VPCSUM_SYNC_EACH_TEST=0 turns it off."""
     yield
-    if os.environ.get("VPCSUM_SYNC_EACH_TEST") == "1" and request.node.get_closest_marker("gpu"):
+    if os.environ.get("VPCSUM_SYNC_EACH_TEST", "1") != "0" and request.node.get_closest_marker("gpu"):
+        import gc
         import torch
-        torch.cuda.synchronize()
+        gc.collect()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
