@@ -1482,11 +1482,14 @@ def test_parse_tuples_match_oracle(V, orc):
     assert nacc > 4000
 
 
-def test_ctx_parse_frames_tuples(V, orc):
+@pytest.mark.parametrize("service", [False, True])
+def test_ctx_parse_frames_tuples(V, orc, service):
     """vpcsum_ctx_parse_frames (PNI parseFrames, GpuCsumBatch.parseFrames): an RX batch in a
     registered arena parsed where it lies, with flow tuples; descriptors, status and tuples equal
     the oracle's, and the descriptors verify the frames through vpcsum_ctx_submit as the
-    reference's recompute does.  Two batches back to back exercise both slots."""
+    reference's recompute does.  Two batches back to back exercise both slots.  service: batches
+    of up to 400 frames parsed on the service grid (svc_frame_packet, parse only), every byte of
+    the results equal to the launched parse kernel's."""
     import edgevec as E
     frames = [f for f, _, _ in E.parse_cases()]
     a, d = orc.synth(600, 2048, 14, O.SYNTH_FUZZ, O.SEED, 99)
@@ -1503,8 +1506,17 @@ def test_ctx_parse_frames_tuples(V, orc):
     n = len(frames)
     ctx = V.Context(0, max_arena=arena.nbytes, max_pkts=n)
     ctx.register(arena)
+    if service:
+        ref = ctx.parse_frames(arena, np.array(offs), np.array(lens))   # launched: n > 512
+        ctx.set_service(20000)
     for rep in range(2):
-        desc, st, tu = ctx.parse_frames(arena, np.array(offs), np.array(lens))
+        if service:
+            parts = [ctx.parse_frames(arena, np.array(offs[lo:lo + 400]), np.array(lens[lo:lo + 400]))
+                     for lo in range(0, n, 400)]
+            desc, st, tu = (np.concatenate([p_[k] for p_ in parts]) for k in range(3))
+            assert desc.tobytes() == ref[0].tobytes() and np.array_equal(st, ref[1]) and tu.tobytes() == ref[2].tobytes()
+        else:
+            desc, st, tu = ctx.parse_frames(arena, np.array(offs), np.array(lens))
         for i, f in enumerate(frames):
             info, _ = O.parse_ether(f)
             w = O.flow_tuple(f)
@@ -1523,6 +1535,8 @@ def test_ctx_parse_frames_tuples(V, orc):
     good = np.ascontiguousarray(desc[ok])
     vout, vst = ctx.run(arena, good, O.MODE_VERIFY)
     want, want_st = orc.process(arena, good, O.MODE_VERIFY)
+    if service:
+        assert ctx.stats()["service_batches"] == 2 * ((n + 399) // 400)
     ctx.close()
     assert np.array_equal(vout, want) and np.array_equal(vst, want_st)
 

@@ -64,6 +64,8 @@ int main(int argc, char** argv) {
     std::vector<uint32_t> flen(nmax);
     std::vector<uint8_t> fflags(nmax, VPCSUM_F_IP | VPCSUM_F_L4);
     std::vector<uint8_t> fst(nmax);
+    std::vector<vpcsum_desc_t> pdesc_out(nmax);
+    std::vector<vpcsum_tuple_t> tup(nmax);
     for (uint32_t i = 0; i < nmax; ++i) {
         uint8_t* f = eth.data() + (size_t)i * stride;
         f[12] = 0x08;
@@ -86,10 +88,12 @@ int main(int argc, char** argv) {
     // 8 = raw frames through the service grid (parse + sum per frame, no launch).
     // 9 / 10 = ingress verify of received frames, status bytes only (vpcsum_ctx_verify_frames, the
     // GpuCsumBatch.verifyFrames form), launched (parse + verify kernels) / service grid.
-    constexpr int kCfg = 11;
+    // 11 / 12 = parse of received frames with flow tuples (vpcsum_ctx_parse_frames), launched / service.
+    constexpr int kCfg = 13;
     static const char* names[kCfg] = {"launch", "service", "service_no_inline", "service_clamped_loads",
                                       "service_release_done", "egress_frames", "pre_launch", "pre_service",
-                                      "egress_frames_service", "verify_frames", "verify_frames_service"};
+                                      "egress_frames_service", "verify_frames", "verify_frames_service",
+                                      "parse_frames", "parse_frames_service"};
     static const uint32_t sizes[7] = {1u, 3u, 4u, 32u, 128u, 1024u, 8192u};
     constexpr int kRounds = 5;
     std::vector<double> us[kCfg][7];
@@ -98,7 +102,7 @@ int main(int argc, char** argv) {
             setenv("VPCSUM_SVC_INLINE", svc == 2 ? "0" : "1", 1);
             setenv("VPCSUM_SVC_CLAMP", svc == 3 ? "1" : "0", 1);
             setenv("VPCSUM_SVC_RELEASE_DONE", svc == 4 ? "1" : "0", 1);
-            if (vpcsum_ctx_set_service(ctx, ((svc && svc < 5) || svc == 7 || svc == 8 || svc == 10) ? 200000 : 0)) {
+            if (vpcsum_ctx_set_service(ctx, ((svc && svc < 5) || svc == 7 || svc == 8 || svc == 10 || svc == 12) ? 200000 : 0)) {
                 fprintf(stderr, "service: %s\n", vpcsum_last_error());
                 return 1;
             }
@@ -108,7 +112,10 @@ int main(int argc, char** argv) {
                 for (int it = 0; it < iters / kRounds + 20; ++it) {
                     uint64_t t = 0;
                     const auto t0 = std::chrono::steady_clock::now();
-                    const int rc = svc >= 9
+                    const int rc = svc >= 11
+                        ? vpcsum_ctx_parse_frames(ctx, eth.data(), eth.size(), foff.data(), flen.data(), b, pdesc_out.data(),
+                                                  fst.data(), tup.data(), &t)
+                        : svc >= 9
                         ? vpcsum_ctx_verify_frames(ctx, eth.data(), eth.size(), foff.data(), flen.data(), b, nullptr,
                                                    fst.data(), &t)
                         : (svc == 5 || svc == 8)

@@ -158,6 +158,11 @@ constexpr uint32_t kZeroCopyWaveTeams = 4096;
 // ~1000 packets on (tools/flush_latency.cpp: 1024 packets 55 us launched vs 58 us through the
 // service, profiles/r05m_flush_latency.json).
 
+// The service's aux buffer: kSvcBatchMax pre-images of 48 B, or kSvcBatchMax descriptors followed
+// by kSvcBatchMax tuples (a parse batch, kSvcParse)
+constexpr size_t kSvcAuxBytes = (size_t)vpcsum::kSvcBatchMax * (sizeof(vpcsum_desc_t) + sizeof(vpcsum_tuple_t));
+static_assert(kSvcAuxBytes >= (size_t)vpcsum::kSvcBatchMax * sizeof(vpcsum_pre_t), "aux buffer holds a batch of pre-images");
+
 // Low-latency service of a context (kernels.hip k_csum_service).
 struct Service {
     vpcsum::SvcMailbox* mb = nullptr;    // host-pinned, coherent (uncached on the GPU), mapped
@@ -173,7 +178,8 @@ struct Service {
     vpcsum_desc_t* dh_desc = nullptr;
     uint32_t* dh_out = nullptr;
     uint8_t* dh_status = nullptr;
-    void* h_pre = nullptr;               // pre-images of a batch with F_PRE frames (kSvcBatchMax x 48 B)
+    void* h_pre = nullptr;               // the aux buffer (kSvcAuxBytes): pre-images of a batch with F_PRE
+                                         // frames, or a parse batch's descriptors and tuples
     void* dh_pre = nullptr;
     uint64_t par[3] = {0, 0, 0};         // arena, arena_len, arena_w last published
     bool par_valid = false;
@@ -505,8 +511,7 @@ int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
             (e = hipHostMalloc((void**)&v.h_desc, (size_t)c->max_pkts * sizeof(vpcsum_desc_t), fl)) != hipSuccess ||
             (e = hipHostMalloc((void**)&v.h_out, (size_t)c->max_pkts * 4, fl)) != hipSuccess ||
             (e = hipHostMalloc((void**)&v.h_status, (size_t)c->max_pkts, fl)) != hipSuccess ||
-            (e = hipHostMalloc((void**)&v.h_pre, (size_t)std::min(c->max_pkts, kSvcBatchMax) * sizeof(vpcsum_pre_t), fl)) !=
-                hipSuccess ||
+            (e = hipHostMalloc((void**)&v.h_pre, kSvcAuxBytes, fl)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&v.dh_pre, v.h_pre, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&v.dh_desc, v.h_desc, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&v.dh_out, v.h_out, 0)) != hipSuccess ||
@@ -758,10 +763,16 @@ static int slot_finish(vpcsum_ctx* c, Slot& s) {
         return 0;
     }
     if (s.kind == 2) {   // parse: descriptors, status and tuples were written to the pinned staging
-        if (s.user_desc_out) memcpy(s.user_desc_out, s.h_desc, (size_t)s.n * sizeof(vpcsum_desc_t));
-        if (s.user_status) memcpy(s.user_status, s.h_status, s.n);
-        if (s.user_tuples) memcpy(s.user_tuples, s.h_tu, (size_t)s.n * sizeof(vpcsum_tuple_t));
+        const bool svc = s.svc_seq != 0;   // or, through the service grid, to its aux buffer
+        const uint8_t* aux = (const uint8_t*)c->svc.h_pre;
+        if (s.user_desc_out)
+            memcpy(s.user_desc_out, svc ? aux : (const uint8_t*)s.h_desc, (size_t)s.n * sizeof(vpcsum_desc_t));
+        if (s.user_status) memcpy(s.user_status, svc ? c->svc.h_status : s.h_status, s.n);
+        if (s.user_tuples)
+            memcpy(s.user_tuples, svc ? aux + (size_t)kSvcBatchMax * sizeof(vpcsum_desc_t) : (const uint8_t*)s.h_tu,
+                   (size_t)s.n * sizeof(vpcsum_tuple_t));
         s.busy = false;
+        s.svc_seq = 0;
         return 0;
     }
     const uint32_t* res_out = s.svc_seq ? c->svc.h_out : s.h_out;
@@ -819,14 +830,15 @@ static int svc_drain(vpcsum_ctx* c) {
 // a time; descriptors (and pre-images) into the service's buffers, the parameter block if it
 // changed, then the command word.  `base` is the device address of h_arena[0].  Caller holds c->mu
 // on c's device; slot s (ticket t) is free.
-// frames: h_desc is the service's own buffer, filled with SvcFrameRec records (egress frames).
+// frames: h_desc is the service's own buffer, filled with SvcFrameRec records (raw frames); parse:
+// the frames are parsed only (vpcsum_ctx_parse_frames).
 static int svc_post(vpcsum_ctx* c, Slot& s, uint64_t t, uint8_t* h_arena, uint64_t arena_len, uint8_t* base,
                     const vpcsum_desc_t* h_desc, uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode,
-                    const void* h_pre, uint32_t pre_fmt, uint64_t* ticket, bool frames = false) {
+                    const void* h_pre, uint32_t pre_fmt, uint64_t* ticket, bool frames = false, bool parse = false) {
     Service& v = c->svc;
     SvcMailbox* mb = v.mb;
     if (!frames) memcpy(v.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
-    uint64_t cmd = frames ? kSvcFrames : 0;
+    uint64_t cmd = (frames ? kSvcFrames : 0) | (parse ? kSvcParse : 0);
     if (h_pre) {
         // the pre-images, each F_PRE frame's stored L4 sum copied into its entry's spare bytes
         // (vpcsum_pre4_t rsv[1..2], vpcsum_pre_t rsv[0..1]): the kernel takes the sum from there,
@@ -1278,6 +1290,28 @@ int vpcsum_ctx_parse_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t ar
                 s.h_tu = s.dh_tu = nullptr;
                 return hipfail(e, "vpcsum_ctx_parse_frames allocation");
             }
+        }
+        if (n && c->svc.on && n <= kSvcBatchMax) {
+            // a small received batch: the service grid parses each frame (kernels.hip svc_frame_packet)
+            if (svc_drain(c) != 0) return -1;
+            SvcFrameRec* r = reinterpret_cast<SvcFrameRec*>(c->svc.h_desc);
+            for (uint32_t i = 0; i < n; ++i) {
+                SvcFrameRec x;
+                memset(&x, 0, sizeof(x));
+                x.off = h_frame_off[i];
+                x.len = h_frame_len[i];
+                x.flags = VPCSUM_F_IP | VPCSUM_F_L4;   // the descriptor flags: the sums each frame allows
+                memcpy(&r[i], &x, sizeof(x));
+            }
+            if (svc_post(c, s, t, const_cast<uint8_t*>(h_arena), arena_len, base, c->svc.h_desc, n, nullptr, h_status, 0,
+                         nullptr, 0, ticket, true, true) != 0)
+                return -1;
+            s.kind = 2;
+            s.user_arena = nullptr;
+            s.user_desc = nullptr;
+            s.user_desc_out = h_desc;
+            s.user_tuples = h_tuples;
+            return 0;
         }
         if (n) {
             // parsed where the frames lie (zero-copy); results straight into the pinned staging

@@ -23,13 +23,14 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
 // no separate descriptor read over PCIe.
 constexpr int kSvcInlineDesc = 3;
 struct alignas(64) SvcMailbox {
-    uint64_t cmd;        // host: seq (bits 0..31, 0 = none yet) | n (32..55) | kSvcFrames | kSvcPre | kSvcPreFmt | kSvcInline |
+    uint64_t cmd;        // host: seq (bits 0..31, 0 = none yet) | n (32..55) | kSvcParse | kSvcFrames | kSvcPre | kSvcPreFmt | kSvcInline |
                          // kSvcStop | kSvcVerify | kSvcParams
     uint64_t rsv0;
     vpcsum_desc_t idesc[kSvcInlineDesc];   // host: descriptors 0..2 of the batch, rsv = (uint8_t)seq
     alignas(64) uint64_t arena;   // line 1, device addresses, read when kSvcParams: arena, then
     uint64_t arena_len, arena_w, desc, out, status, opts, pre;   // opts: kSvcOpt* (tooling); pre: the
-                                                                 // service's pre-image buffer (kSvcPre batches)
+                                                                 // service's aux buffer: pre-images (kSvcPre
+                                                                 // batches) or parse results (kSvcParse)
     alignas(64) uint32_t done;   // device: last completed batch
     uint32_t pad_;
     uint64_t stamp[7];           // VPCSUM_SVC_STAMPS builds only: s_memrealtime per batch step
@@ -45,6 +46,9 @@ constexpr uint64_t kSvcPre = 1ull << 58, kSvcPreFmt = 1ull << 59;
 // a batch of raw egress frames (vpcsum_ctx_egress_frames): the descriptor buffer (and the inline
 // descriptors) hold SvcFrameRec records, each frame is parsed on the GPU before it is summed
 constexpr uint64_t kSvcFrames = 1ull << 57;
+// with kSvcFrames: parse only (vpcsum_ctx_parse_frames) -- descriptors at the aux buffer's start,
+// tuples after kSvcBatchMax descriptors, status bytes; no sums
+constexpr uint64_t kSvcParse = 1ull << 56;
 struct SvcFrameRec {
     uint64_t off;    // the frame's offset in the arena
     uint32_t len;    // its length

@@ -333,6 +333,7 @@ __device__ __forceinline__ void svc_pre_packet(const uint8_t* __restrict__ arena
 
 __device__ __forceinline__ uint8_t parse_frame(const uint8_t* f, uint64_t o, uint32_t L, bool ok, uint8_t w, bool egress,
                                                vpcsum_desc_t& d);
+__device__ __forceinline__ void frame_tuple(const uint8_t* b, const vpcsum_desc_t& d, uint32_t st, uint32_t t[10]);
 
 // A raw frame on the service grid, one wave per frame: an egress frame (vpcsum_ctx_egress_frames)
 // or, VERIFY, a received one (vpcsum_ctx_verify_frames).  Its first 384 B (every byte parse_frame
@@ -342,11 +343,13 @@ __device__ __forceinline__ uint8_t parse_frame(const uint8_t* f, uint64_t o, uin
 // where the launched path runs a parse kernel and a checksum kernel.  rec: the frame's 16-B record
 // {u64 offset; u32 length; u8 flags; ...}.
 constexpr int kSvcFrameChunks = 25;   // 384 B at any offset within a 16-B chunk
-template <bool VERIFY, bool PRED>
+// PARSE (vpcsum_ctx_parse_frames): no sums; lane 0 writes the frame's descriptor to aux[p] and its
+// flow tuple to the tuple array after kSvcBatchMax descriptors (frame_tuple, from the staged bytes).
+template <bool VERIFY, bool PRED, bool PARSE = false>
 __device__ __forceinline__ void svc_frame_packet(const uint8_t* __restrict__ arena, uint64_t arena_len, const uint4 rec,
                                                  const uint32_t p, uint32_t* __restrict__ out,
                                                  uint8_t* __restrict__ status, uint8_t* __restrict__ arena_w,
-                                                 const int tl) {
+                                                 const int tl, void* __restrict__ aux = nullptr) {
     __shared__ uint4 s_fw[4][kSvcFrameChunks];
     const int wv = (threadIdx.x >> 6) & 3;
     const uint64_t o = (uint64_t)rec.x | ((uint64_t)rec.y << 32);
@@ -364,10 +367,21 @@ __device__ __forceinline__ void svc_frame_packet(const uint8_t* __restrict__ are
     uint32_t st = VPCSUM_S_BAD_DESC;
     if (tl == 0) {
         vpcsum_desc_t d;
-        st = parse_frame((const uint8_t*)&s_fw[wv][0] + r0, o, L, inb, (uint8_t)(rec.w & 0xffu), !VERIFY, d);
+        const uint8_t* fb = (const uint8_t*)&s_fw[wv][0] + r0;
+        st = parse_frame(fb, o, L, inb, (uint8_t)(rec.w & 0xffu), !VERIFY && !PARSE, d);
         dd = make_uint4((uint32_t)d.l3_off, (uint32_t)(d.l3_off >> 32), (uint32_t)d.l3_len | ((uint32_t)d.l4_off << 16),
                         (uint32_t)d.l3_ver | ((uint32_t)d.l4_proto << 8) | ((uint32_t)d.flags << 16));
+        if constexpr (PARSE) {
+            // the descriptor, the status byte and the tuple straight to the host's buffers
+            uint32_t t[10];
+            frame_tuple(fb + (st == 0 ? (int)(d.l3_off - o) : 0), d, st, t);
+            ((uint4*)aux)[p] = dd;
+            uint32_t* tp = (uint32_t*)((uint8_t*)aux + (size_t)kSvcBatchMax * sizeof(vpcsum_desc_t)) + (size_t)p * 10;
+            for (int k = 0; k < 10; ++k) tp[k] = t[k];
+            if (status) status[p] = (uint8_t)st;
+        }
     }
+    if constexpr (PARSE) return;
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");   // s_fw is the next frame's
     dd = shfl_u4(dd, 0);
@@ -388,7 +402,8 @@ __device__ __forceinline__ void svc_frame_packet(const uint8_t* __restrict__ are
 // on uncached host memory (zero-copy frames) every such load is another PCIe read.
 // SVC (the service grid, TEAM 64): 1 = F_PRE descriptors take svc_pre_packet with the pre-images
 // at `pre` (fmt 0: vpcsum_pre4_t, 1: vpcsum_pre_t; without `pre` they are no-ops, as everywhere
-// else); 2 = `desc` holds raw frame records (svc_frame_packet).
+// else); 2 = `desc` holds raw frame records (svc_frame_packet); 3 = the same, parse only (descriptors
+// and tuples into the aux buffer at `pre`).
 template <int TEAM, int U, bool VERIFY, bool NT, bool PRED = false, int SVC = 0>
 __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
@@ -417,6 +432,8 @@ __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64
         }
         if constexpr (SVC == 2) {
             svc_frame_packet<VERIFY, PRED>(arena, arena_len, dv, p, out, status, arena_w, tl);
+        } else if constexpr (SVC == 3) {
+            svc_frame_packet<false, PRED, true>(arena, arena_len, dv, p, out, status, arena_w, tl, const_cast<void*>(pre));
         } else {
             if constexpr (SVC == 1) {
                 if (pre && (((dv.w >> 16) & 0xffu) & VPCSUM_F_PRE)) {
@@ -1455,7 +1472,8 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         uint8_t* status = (uint8_t*)s_par[5];
         const bool pred = (s_par[6] & kSvcOptClampLoads) == 0;
         const bool rel_done = (s_par[6] & kSvcOptReleaseDone) != 0;
-        const void* pre = (cmd & kSvcPre) ? (const void*)s_par[7] : nullptr;
+        const void* s_aux = (const void*)s_par[7];   // the aux buffer: pre-images, or parse results
+        const void* pre = (cmd & kSvcPre) ? s_aux : nullptr;
         const int pre_fmt = (cmd & kSvcPreFmt) ? 1 : 0;
         __syncthreads();   // s_cmd / s_par are rewritten next round
         if (cmd == 0) return;
@@ -1473,6 +1491,9 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                 k1_run<64, 4, true, true, true, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
             else if (cmd & kSvcVerify)
                 k1_run<64, 4, true, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+            else if ((cmd & kSvcFrames) && (cmd & kSvcParse))
+                k1_run<64, 4, false, true, true, 3>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x,
+                                                    gridDim.x, (const void*)s_aux);
             else if (cmd & kSvcFrames)
                 k1_run<64, 4, false, true, true, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
             else
@@ -1483,6 +1504,9 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                 k1_run<64, 4, true, true, false, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
             else if (cmd & kSvcVerify)
                 k1_run<64, 4, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+            else if ((cmd & kSvcFrames) && (cmd & kSvcParse))
+                k1_run<64, 4, false, true, false, 3>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x,
+                                                     gridDim.x, (const void*)s_aux);
             else if (cmd & kSvcFrames)
                 k1_run<64, 4, false, true, false, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
             else
@@ -1854,6 +1878,36 @@ __device__ __forceinline__ uint8_t parse_frame(const uint8_t* f, uint64_t o, uin
     return st;
 }
 
+// The flow tuple the L4 input nodes read (vpcsum.h vpcsum_tuple_t) of a parsed frame, from its L3
+// bytes at b: addresses at Ipv4Packet :51-54 (12, 16) / Ipv6Packet :47-50 (8, 24), ports and TCP
+// flags at TcpPacket / UdpPacket.initPartial (0, 2, 12); zeros for a refused frame (st != 0).
+__device__ __forceinline__ void frame_tuple(const uint8_t* b, const vpcsum_desc_t& d, uint32_t st, uint32_t t[10]) {
+    for (int k = 0; k < 10; ++k) t[k] = 0;
+    if (st != 0) return;
+    auto put = [&](int dw0, const uint8_t* src, int nb) {   // bytes in memory order
+        if (!((uintptr_t)src & 1)) {   // halfword loads where the field is 2-B aligned
+            const uint16_t* h = (const uint16_t*)src;
+            for (int k = 0; k < nb / 2; ++k) t[dw0 + (k >> 1)] |= (uint32_t)h[k] << (16 * (k & 1));
+        } else {
+            for (int k = 0; k < nb; ++k) t[dw0 + (k >> 2)] |= (uint32_t)src[k] << (8 * (k & 3));
+        }
+    };
+    if (d.l3_ver == 4) {
+        put(0, b + 12, 4);
+        put(4, b + 16, 4);
+    } else {
+        put(0, b + 8, 16);
+        put(4, b + 24, 16);
+    }
+    const uint8_t* l4 = b + d.l4_off;
+    uint32_t w8 = d.l3_ver | ((uint32_t)d.l4_proto << 8);
+    if (d.l4_proto == 6 || d.l4_proto == 17) {   // accepted: at least 8 / 20 bytes
+        put(8, l4, 4);
+        if (d.l4_proto == 6) w8 |= (uint32_t)(l4[13] & 0x3f) << 16;
+    }
+    t[9] = w8;
+}
+
 __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                     const uint64_t* __restrict__ foff,
                                                     const uint32_t* __restrict__ flen, uint32_t n, uint8_t want,
@@ -1882,32 +1936,8 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
             // the flow tuple the L4 input nodes read (vpcsum.h vpcsum_tuple_t): addresses at
             // Ipv4Packet :51-54 (12, 16) / Ipv6Packet :47-50 (8, 24), ports and TCP flags at
             // TcpPacket / UdpPacket.initPartial (0, 2, 12); zeros for a refused frame
-            uint32_t t[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-            if (st == 0) {
-                const uint8_t* b = arena + d.l3_off;
-                auto put = [&](int dw0, const uint8_t* src, int nb) {   // bytes in memory order
-                    if (!((uintptr_t)src & 1)) {   // halfword loads where the field is 2-B aligned
-                        const uint16_t* h = (const uint16_t*)src;
-                        for (int k = 0; k < nb / 2; ++k) t[dw0 + (k >> 1)] |= (uint32_t)h[k] << (16 * (k & 1));
-                    } else {
-                        for (int k = 0; k < nb; ++k) t[dw0 + (k >> 2)] |= (uint32_t)src[k] << (8 * (k & 3));
-                    }
-                };
-                if (d.l3_ver == 4) {
-                    put(0, b + 12, 4);
-                    put(4, b + 16, 4);
-                } else {
-                    put(0, b + 8, 16);
-                    put(4, b + 24, 16);
-                }
-                const uint8_t* l4 = b + d.l4_off;
-                uint32_t w8 = d.l3_ver | ((uint32_t)d.l4_proto << 8);
-                if (d.l4_proto == 6 || d.l4_proto == 17) {   // accepted: at least 8 / 20 bytes
-                    put(8, l4, 4);
-                    if (d.l4_proto == 6) w8 |= (uint32_t)(l4[13] & 0x3f) << 16;
-                }
-                t[9] = w8;
-            }
+            uint32_t t[10];
+            frame_tuple(arena + d.l3_off, d, st, t);
             uint32_t* wt = s_tu + (threadIdx.x & ~63u) * 10;   // this wave's 64 x 10 dwords
             for (int k = 0; k < 10; ++k) wt[ln * 10 + k] = t[k];
             wave_sync_lds();
