@@ -547,3 +547,81 @@ def test_full_size_c5_preimage(V, orc):
     orc.nat4_java(a, dd, np.ascontiguousarray(rw.numpy().view(O.NAT4_DTYPE).reshape(-1)[i0:i0 + 4096]))
     assert np.array_equal(arena[i0 * stride:(i0 + 4096) * stride].cpu().numpy(), a)
     del arena, fr
+
+
+@pytest.mark.parametrize("idle_us", [5000, 40])
+def test_service_mixed_forms(V, orc, idle_us):
+    """One context with the service grid on, two registered arenas (raw Ethernet frames as the TX /
+    RX rings hold them, and NAT'd C5-like frames with pre-images), and a random sequence of every
+    batch form the grid takes -- descriptor flushes in all three modes, raw egress frames, RX verify
+    with and without sums, RX parse with tuples, pre-image flushes -- of 1..600 frames (above 512:
+    launched): after every batch the results and both arenas equal a twin context's without the
+    service (the launched kernels, each pinned to the oracle by the tests above).  Catches state
+    carried from one form to the next: the command flags, the parameter block switching arenas and
+    write modes, the aux buffer shared by pre-images and parse results."""
+    import sys
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import egressvec as E
+    rng = np.random.default_rng(70 + idle_us)
+    fs = E.frames()
+    ea, offs = E.layout(fs)
+    flags = [E.want_flags(f["ver"], f["proto"], i) for i, f in enumerate(fs)]
+    edesc = E.oracle_descriptors(fs, offs, flags)
+    offs = np.array(offs, np.uint64)
+    lens = np.array([len(f["frame"]) for f in fs], np.uint32)
+    fflags = np.array(flags, np.uint8)
+    after, ndesc, pre, _, _ = nat_case(orc, rng, 700, O.SYNTH_C5, pad=14, stride=2048, udp_zero=0.1, mask=NAT_FIELDS)
+    full = rng.random(len(ndesc)) < 0.3
+    ndesc["flags"][full] &= 0xFF ^ O.F_PRE
+    arenas = {"svc": (ea.copy(), after.copy()), "ref": (ea.copy(), after.copy())}
+    ctxs = {}
+    for k, (a1, a2) in arenas.items():
+        c = V.Context(0, max_arena=max(a1.nbytes, a2.nbytes), max_pkts=1024)
+        c.register(a1)
+        c.register(a2)
+        if k == "svc":
+            c.set_service(idle_us)
+        ctxs[k] = c
+    n_svc = 0
+    for it in range(60):
+        form = str(rng.choice(["submit", "egress", "verify", "verify_st", "parse", "pre"]))
+        b = int(rng.choice([1, 3, 5, 32, 200, 512, 600]))
+        res = {}
+        for k in ("svc", "ref"):
+            c, (a1, a2) = ctxs[k], arenas[k]
+            r2 = np.random.default_rng(it)                      # the same subset for both contexts
+            if form == "pre":
+                idx = np.sort(r2.choice(len(ndesc), b, replace=False))
+                d = np.ascontiguousarray(ndesc[idx])
+                res[k] = c.run_pre(a2, d, np.ascontiguousarray(pre[idx]), O.MODE_WRITE)
+            elif form == "submit":
+                idx = np.sort(r2.choice(len(edesc), min(b, len(edesc)), replace=False))
+                mode = int(r2.choice([O.MODE_COMPUTE, O.MODE_VERIFY, O.MODE_WRITE]))
+                out = np.zeros(len(idx), np.uint32)
+                st = np.zeros(len(idx), np.uint8)
+                c.wait(c.submit(a1, np.ascontiguousarray(edesc[idx]), out, st, mode))
+                res[k] = (out, st)
+            else:
+                idx = r2.choice(len(fs), min(b, len(fs)), replace=False)
+                if form == "egress":
+                    res[k] = c.egress_frames(a1, offs[idx], lens[idx], fflags[idx])
+                elif form == "parse":
+                    dd, st, tu = c.parse_frames(a1, offs[idx], lens[idx])
+                    res[k] = (dd.tobytes(), st, tu.tobytes())
+                else:
+                    res[k] = c.verify_frames(a1, offs[idx], lens[idx], sums=form == "verify")
+        what = f"it {it} form {form} n {b}"
+        for x, y in zip(res["svc"], res["ref"]):
+            if x is None or isinstance(x, bytes):
+                assert x == y, what
+            else:
+                assert np.array_equal(x, y), what
+        assert np.array_equal(arenas["svc"][0], arenas["ref"][0]) and np.array_equal(arenas["svc"][1], arenas["ref"][1]), what
+        n_svc += b <= 512 if form == "pre" else min(b, len(fs)) <= 512
+        t_end = time.perf_counter() + float(rng.integers(0, 3 * idle_us)) * 1e-6
+        while time.perf_counter() < t_end:
+            pass
+    assert ctxs["svc"].stats()["service_batches"] == n_svc and ctxs["ref"].stats()["service_batches"] == 0
+    for c in ctxs.values():
+        c.close()
