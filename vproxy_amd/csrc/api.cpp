@@ -186,6 +186,7 @@ struct Service {
     uint32_t posted = 0;                 // last batch published (seq)
     uint64_t idle_ticks = 0;             // 100 MHz ticks
     bool on = false;
+    std::chrono::steady_clock::time_point last_post;   // the last batch posted (svc_quiesce)
     bool inline_desc = true;             // descriptors of <= kSvcInlineDesc frames ride in the command line
                                          // (VPCSUM_SVC_INLINE=0 turns it off: A/B tooling)
 #ifdef VPCSUM_SVC_STAMPS
@@ -826,6 +827,24 @@ static int svc_drain(vpcsum_ctx* c) {
     return 0;
 }
 
+// Before a launched zero-copy batch (more than kSvcBatchMax frames, or a form the grid does not
+// take): a resident service grid that has had no batch for kSvcKeep is stopped first -- it leaves
+// after its current poll -- and the next small batch relaunches it (svc_post).  With an idle grid
+// resident, launched zero-copy batches ran 6-50% slower (tools/flush_latency.cpp: 1,024 parsed
+// frames 36.6 vs 24.5 us); a small batch right after a stop pays a grid launch (32 frames 29 us
+// instead of 13.5), hence the grace period: traffic that alternates small and large batches keeps
+// its grid, a phase of large batches runs without one.
+constexpr auto kSvcKeep = std::chrono::microseconds(1000);
+static int svc_quiesce(vpcsum_ctx* c) {
+    Service& v = c->svc;
+    if (!v.on || hipStreamQuery(v.stream) == hipSuccess) return 0;   // off, or no grid resident
+    if (std::chrono::steady_clock::now() - v.last_post < kSvcKeep) return 0;
+    if (svc_drain(c) != 0) return -1;
+    __atomic_store_n(&v.mb->cmd, kSvcStop | v.posted, __ATOMIC_RELEASE);
+    VPC_CHECK(hipStreamSynchronize(v.stream), "service stop");
+    return 0;
+}
+
 // Hand a zero-copy batch to the low-latency service (c->svc.on, n <= kSvcBatchMax): one batch at
 // a time; descriptors (and pre-images) into the service's buffers, the parameter block if it
 // changed, then the command word.  `base` is the device address of h_arena[0].  Caller holds c->mu
@@ -888,6 +907,7 @@ static int svc_post(vpcsum_ctx* c, Slot& s, uint64_t t, uint8_t* h_arena, uint64
 #endif
     __atomic_store_n(&mb->cmd, cmd, __ATOMIC_RELEASE);
     v.posted = seq;
+    v.last_post = std::chrono::steady_clock::now();
     ++c->svc_batches;
     if (hipStreamQuery(v.stream) == hipSuccess && svc_launch(c, seq - 1) != 0) return -1;
     s.zero_copy = true;
@@ -943,6 +963,7 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, con
                 if (svc_drain(c) != 0) return -1;
                 return svc_post(c, s, t, h_arena, arena_len, base, h_desc, n, h_out, h_status, mode, nullptr, 0, ticket);
             }
+            if (svc_quiesce(c) != 0) return -1;
             memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
             // up to kZeroCopyWaveTeams packets: one wave per packet (variant 12, 64 lanes x 4
             // predicated loads), so the batch is a few PCIe round trips deep instead of K2's per-unit
@@ -1058,6 +1079,7 @@ int vpcsum_ctx_submit_pre(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len,
         memcpy(s.h_rw, h_pre, (size_t)n * esz);
         if (dev_arena) {
             // registered arena (umem): in place; an F_PRE packet's header is all that crosses PCIe
+            if (svc_quiesce(c) != 0) return -1;
             uint8_t* base = dev_arena - lo;
             memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
             if (full)
@@ -1176,6 +1198,7 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
         }
         if (n) {
             // parse the frames where they lie (zero-copy), then verify the descriptors it built
+            if (svc_quiesce(c) != 0) return -1;
             memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
             memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
             VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.d_desc,
@@ -1238,6 +1261,7 @@ int vpcsum_ctx_egress_frames(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_l
             return 0;
         }
         if (n) {
+            if (svc_quiesce(c) != 0) return -1;
             // the frames' own flags ride in the status staging: the parse reads them before the
             // checksum kernel, later on the same stream, overwrites them with the statuses
             memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
@@ -1315,6 +1339,7 @@ int vpcsum_ctx_parse_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t ar
         }
         if (n) {
             // parsed where the frames lie (zero-copy); results straight into the pinned staging
+            if (svc_quiesce(c) != 0) return -1;
             memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
             memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
             VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.dh_desc,
@@ -1366,6 +1391,7 @@ int vpcsum_ctx_nat_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len,
         memcpy(s.h_rw, h_rw, (size_t)n * sizeof(vpcsum_nat_t));
         if (dev_arena) {
             // the frames live in a registered (page-locked, mapped) arena: rewritten where they lie
+            if (svc_quiesce(c) != 0) return -1;
             memcpy(s.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
             if (n && nat_run(dev_arena - lo, arena_len, s.dh_desc, s.dh_rw, 1, n, s.dh_status, nat_mode, s.stream) != 0)
                 return -1;
