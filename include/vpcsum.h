@@ -305,11 +305,14 @@ int vpcsum_ctx_submit(vpcsum_ctx_t* ctx, uint8_t* h_arena, uint64_t arena_len,
                       const vpcsum_desc_t* h_desc, uint32_t n,
                       uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket);
 int vpcsum_ctx_wait(vpcsum_ctx_t* ctx, uint64_t ticket);
-/* Low-latency flushes (idle_us > 0): submits from a registered (zero-copy) arena are handed to a
- * small persistent grid that polls a pinned mailbox, instead of a kernel launch + event wait per
- * batch -- the Iface.completeTx flush of a few dozen frames (XDPIface.java:227-243).  Batches
- * then run one at a time.  The grid leaves after idle_us without a batch and is restarted by
- * the next submit.  idle_us = 0 stops it (the default).  Other submits are unaffected. */
+/* Low-latency flushes (idle_us > 0): zero-copy batches of up to 512 frames from a registered arena
+ * -- vpcsum_ctx_submit, vpcsum_ctx_submit_pre, vpcsum_ctx_egress_frames, vpcsum_ctx_verify_frames,
+ * vpcsum_ctx_parse_frames -- are handed to a small persistent grid that polls a pinned mailbox,
+ * instead of a kernel launch + event wait per batch (the Iface.completeTx flush of a few dozen
+ * frames, XDPIface.java:227-243, and the RX poll).  Batches then run one at a time.  The grid leaves
+ * after idle_us without a batch and is restarted by the next one; a larger zero-copy batch, which is
+ * launched, first stops a grid that has had no batch for 1 ms.  idle_us = 0 stops it (the
+ * default).  Staged submits are unaffected. */
 int vpcsum_ctx_set_service(vpcsum_ctx_t* ctx, uint32_t idle_us);
 /* Counters of a context: batches the service ran, service grids launched (either may be NULL). */
 int vpcsum_ctx_stats(vpcsum_ctx_t* ctx, uint64_t* service_batches, uint64_t* service_launches);
