@@ -925,6 +925,31 @@ static int svc_post(vpcsum_ctx* c, Slot& s, uint64_t t, uint8_t* h_arena, uint64
     return 0;
 }
 
+// A small batch of raw frames (egress, RX verify or RX parse) to the service grid: one SvcFrameRec
+// per frame in the service's descriptor buffer -- offset, length, and the frame's own flags
+// (h_flags) or `flags` for all -- then svc_post.  The results stay in the service's buffers until
+// slot_finish hands them over; the frames themselves are written in place through the mapping.
+static int svc_post_frames(vpcsum_ctx* c, Slot& s, uint64_t t, const uint8_t* h_arena, uint64_t arena_len, uint8_t* base,
+                           const uint64_t* h_off, const uint32_t* h_len, const uint8_t* h_flags, uint8_t flags,
+                           uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode, bool parse, uint64_t* ticket) {
+    if (svc_drain(c) != 0) return -1;
+    SvcFrameRec* r = reinterpret_cast<SvcFrameRec*>(c->svc.h_desc);
+    for (uint32_t i = 0; i < n; ++i) {
+        SvcFrameRec x;
+        memset(&x, 0, sizeof(x));
+        x.off = h_off[i];
+        x.len = h_len[i];
+        x.flags = h_flags ? h_flags[i] : flags;
+        memcpy(&r[i], &x, sizeof(x));
+    }
+    if (svc_post(c, s, t, const_cast<uint8_t*>(h_arena), arena_len, base, c->svc.h_desc, n, h_out, h_status, mode, nullptr,
+                 0, ticket, true, parse) != 0)
+        return -1;
+    s.user_arena = nullptr;
+    s.user_desc = nullptr;
+    return 0;
+}
+
 int vpcsum_ctx_submit(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const vpcsum_desc_t* h_desc, uint32_t n,
                       uint32_t* h_out, uint8_t* h_status, uint32_t mode, uint64_t* ticket) {
     try {
@@ -1179,22 +1204,8 @@ int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t a
         if (n && c->svc.on && n <= kSvcBatchMax) {
             // a small received batch: the service grid parses and verifies each frame
             // (kernels.hip svc_frame_packet), the sums into its own buffer (copied out only with h_out)
-            if (svc_drain(c) != 0) return -1;
-            SvcFrameRec* r = reinterpret_cast<SvcFrameRec*>(c->svc.h_desc);
-            for (uint32_t i = 0; i < n; ++i) {
-                SvcFrameRec x;
-                memset(&x, 0, sizeof(x));
-                x.off = h_frame_off[i];
-                x.len = h_frame_len[i];
-                x.flags = VPCSUM_F_IP | VPCSUM_F_L4;   // ingress: the sums each frame allows
-                memcpy(&r[i], &x, sizeof(x));
-            }
-            if (svc_post(c, s, t, const_cast<uint8_t*>(h_arena), arena_len, base, c->svc.h_desc, n, h_out, h_status,
-                         VPCSUM_MODE_VERIFY, nullptr, 0, ticket, true) != 0)
-                return -1;
-            s.user_arena = nullptr;
-            s.user_desc = nullptr;
-            return 0;
+            return svc_post_frames(c, s, t, h_arena, arena_len, base, h_frame_off, h_frame_len, nullptr,
+                                   VPCSUM_F_IP | VPCSUM_F_L4, n, h_out, h_status, VPCSUM_MODE_VERIFY, false, ticket);
         }
         if (n) {
             // parse the frames where they lie (zero-copy), then verify the descriptors it built
@@ -1243,22 +1254,8 @@ int vpcsum_ctx_egress_frames(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_l
         if (s.busy && slot_finish(c, s) != 0) return -1;
         if (n && c->svc.on && n <= kSvcBatchMax) {
             // a small flush: the service grid parses and sums each frame (kernels.hip svc_frame_packet)
-            if (svc_drain(c) != 0) return -1;
-            SvcFrameRec* r = reinterpret_cast<SvcFrameRec*>(c->svc.h_desc);
-            for (uint32_t i = 0; i < n; ++i) {
-                SvcFrameRec x;
-                memset(&x, 0, sizeof(x));
-                x.off = h_frame_off[i];
-                x.len = h_frame_len[i];
-                x.flags = h_frame_flags[i];
-                memcpy(&r[i], &x, sizeof(x));
-            }
-            if (svc_post(c, s, t, h_arena, arena_len, base, c->svc.h_desc, n, h_out, h_status, VPCSUM_MODE_WRITE, nullptr, 0,
-                         ticket, true) != 0)
-                return -1;
-            s.user_arena = nullptr;   // written in place through the mapping
-            s.user_desc = nullptr;
-            return 0;
+            return svc_post_frames(c, s, t, h_arena, arena_len, base, h_frame_off, h_frame_len, h_frame_flags, 0, n, h_out,
+                                   h_status, VPCSUM_MODE_WRITE, false, ticket);
         }
         if (n) {
             if (svc_quiesce(c) != 0) return -1;
@@ -1317,22 +1314,10 @@ int vpcsum_ctx_parse_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t ar
         }
         if (n && c->svc.on && n <= kSvcBatchMax) {
             // a small received batch: the service grid parses each frame (kernels.hip svc_frame_packet)
-            if (svc_drain(c) != 0) return -1;
-            SvcFrameRec* r = reinterpret_cast<SvcFrameRec*>(c->svc.h_desc);
-            for (uint32_t i = 0; i < n; ++i) {
-                SvcFrameRec x;
-                memset(&x, 0, sizeof(x));
-                x.off = h_frame_off[i];
-                x.len = h_frame_len[i];
-                x.flags = VPCSUM_F_IP | VPCSUM_F_L4;   // the descriptor flags: the sums each frame allows
-                memcpy(&r[i], &x, sizeof(x));
-            }
-            if (svc_post(c, s, t, const_cast<uint8_t*>(h_arena), arena_len, base, c->svc.h_desc, n, nullptr, h_status, 0,
-                         nullptr, 0, ticket, true, true) != 0)
+            if (svc_post_frames(c, s, t, h_arena, arena_len, base, h_frame_off, h_frame_len, nullptr,
+                                VPCSUM_F_IP | VPCSUM_F_L4, n, nullptr, h_status, 0, true, ticket) != 0)
                 return -1;
             s.kind = 2;
-            s.user_arena = nullptr;
-            s.user_desc = nullptr;
             s.user_desc_out = h_desc;
             s.user_tuples = h_tuples;
             return 0;
