@@ -625,3 +625,57 @@ def test_service_mixed_forms(V, orc, idle_us):
     assert ctxs["svc"].stats()["service_batches"] == n_svc and ctxs["ref"].stats()["service_batches"] == 0
     for c in ctxs.values():
         c.close()
+
+
+def test_service_grids_of_four_contexts_in_threads(V, orc):
+    """Four switches' contexts in four threads (one context per event loop, thread-safe
+    across them), each with its own service grid resident at once, each flushing its own umem:
+    descriptor flushes (WRITE), NAT'd flushes from pre-images and RX verifies of random sizes.  Every
+    result equals the oracle's (Java's bytes for the NAT'd frames)."""
+    import threading
+    ctxs, errors = [], []
+
+    def work(k):
+        try:
+            rng = np.random.default_rng(90 + k)
+            after, desc, pre, want, wst = nat_case(orc, rng, 400, O.SYNTH_C5, pad=14, stride=2048, mask=NAT_FIELDS)
+            arena = after.copy()
+            c = V.Context(0, max_arena=arena.nbytes, max_pkts=512)
+            ctxs.append(c)
+            c.register(arena)
+            c.set_service(5000)
+            live = desc["flags"] != 0
+            for it in range(25):
+                b = int(rng.choice([1, 4, 32, 200, 400]))
+                idx = np.sort(rng.choice(len(desc), b, replace=False))
+                arena[:] = after
+                d = np.ascontiguousarray(desc[idx])
+                out, st = c.run_pre(arena, d, np.ascontiguousarray(pre[idx]), O.MODE_WRITE)
+                for j, i in enumerate(idx):
+                    if live[i]:
+                        o, L = int(desc[i]["l3_off"]), int(desc[i]["l3_len"])
+                        if not np.array_equal(arena[o:o + L], want[o:o + L]) or st[j] != O.S_DONE:
+                            errors.append((k, it, int(i)))
+                            return
+                # the same frames, now Java's bytes, verified: every live packet's stored sums are right
+                vd = np.ascontiguousarray(desc[idx])
+                vd["flags"] = np.where(vd["flags"] != 0, vd["flags"] & (O.F_IP | O.F_L4), O.F_IP | O.F_L4)
+                _, vst = c.run(arena, vd, O.MODE_VERIFY)
+                for j, i in enumerate(idx):
+                    if live[i] and ((vst[j] & O.S_L4_OK) == 0 or ((vd[j]["flags"] & O.F_IP) and (vst[j] & O.S_IP_OK) == 0)):
+                        errors.append((k, it, int(i), "verify"))
+                        return
+        except Exception as e:   # reported by the main thread
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    try:
+        assert not errors, errors[:4]
+        assert len(ctxs) == 4 and all(c.stats()["service_batches"] == 50 for c in ctxs)
+    finally:
+        for c in ctxs:
+            c.close()
