@@ -287,6 +287,42 @@ def parse_cases() -> list[tuple[bytes, bool, str]]:
                         (bytes(2) + inner_arp[:30], False, "inner arp truncated"),
                         (bytes(2) + bytes(12) + b"\x08\x00" + rnd(10), True, "inner ipv4 garbage")):
         cases.append((eth4 + v4(97, l4), ok, f"etherip {why}"))
+    # L3 header rules, IPv4 (Ipv4Packet.initPartial, Ipv4Packet.java:29-63): the buffer, IHL and
+    # totalLength; a shorter totalLength cuts the Ethernet padding off
+    p4 = v4(6, tcp(20))
+    cases.append((eth4 + p4[:19], False, "ipv4 19 B"))
+    for ihl, ok in ((4, False), (0, False), (6, True)):
+        q = bytearray(v4(6, tcp(40)))
+        q[0] = 0x40 | ihl
+        cases.append((eth4 + bytes(q), ok, f"ipv4 ihl {ihl} (tcp at 4*ihl)"))
+    q = bytearray(v4(6, tcp(40)))
+    q[0] = 0x4F                                 # 60-B header in a 60-B packet: no room for TCP
+    _put16(q, 2, 60)
+    cases.append((eth4 + bytes(q), False, "ipv4 ihl 15, totalLength 60"))
+    q = bytearray(p4)
+    q[0] = 0x4F
+    _put16(q, 2, 40)
+    cases.append((eth4 + bytes(q), False, "ipv4 ihl 15 > 40-B buffer"))
+    for total, ok, why in ((24, False, "totalLength < 4*ihl + tcp"), (19, False, "totalLength < 4*ihl"),
+                           (41, False, "totalLength > buffer"), (40, True, "totalLength == buffer")):
+        q = bytearray(p4)
+        _put16(q, 2, total)
+        cases.append((eth4 + bytes(q), ok, f"ipv4 {why}"))
+    cases.append((eth4 + p4 + rnd(6), True, "ipv4 + 6 B ethernet padding"))
+    cases.append((eth4 + v4(17, udp(8)) + bytes(18), True, "ipv4 udp 8 B + 18 B padding"))
+    # IPv6 (Ipv6Packet.initPartial, Ipv6Packet.java:26-59): payloadLength 0 is a jumbogram,
+    # refused; a payload past the buffer refused; padding cut
+    p6 = v6(6, tcp(20))
+    cases.append((eth6 + p6[:39], False, "ipv6 39 B"))
+    for pl, ok, why in ((0, False, "payloadLength 0 (jumbo)"), (21, False, "payloadLength > buffer"),
+                        (19, False, "payloadLength < tcp header")):
+        q = bytearray(p6)
+        _put16(q, 4, pl)
+        cases.append((eth6 + bytes(q), ok, f"ipv6 {why}"))
+    cases.append((eth6 + p6 + rnd(4), True, "ipv6 + 4 B padding"))
+    q = bytearray(v6(17, udp(30), ext=2))
+    _put16(q, 4, 0)
+    cases.append((eth6 + bytes(q), False, "ipv6 ext, payloadLength 0 (jumbo)"))
     # L2: Ethernet / 802.1Q lengths, non-IP types
     cases.append((eth4[:13], False, "ethernet 13 B"))
     cases.append((bytes(12) + b"\x81\x00" + b"\x00\x05", False, "802.1q 16 B"))
