@@ -41,7 +41,7 @@ for b in range(nb):
 torch.cuda.synchronize()
 nbytes = algorithmic_bytes(V.tensor_to_desc(descs[0]))
 out = torch.zeros(n, dtype=torch.int32, device="cuda")
-st = torch.zeros(n, dtype=torch.uint8, device="cuda") if args.mode == 1 else None
+st = torch.zeros(n, dtype=torch.uint8, device="cuda") if args.mode & 1 else None
 ref = torch.zeros(n, dtype=torch.int32, device="cuda")
 variants = [(int(t), int(b)) for t in args.teams.split(",") for b in args.bpc.split(",")]
 V.compute(arenas[1], descs[1], n, ref, None, 0, 4)
