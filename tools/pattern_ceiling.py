@@ -1,5 +1,5 @@
 """Per-workload read ceiling of the frame layout: k_pattern_probe reads exactly K2's chunks
-(descriptors included, no results written, no checksum work).  Prints both as algorithmic
+(--stride=N: another frame stride; descriptors included, no results written, no checksum work).  Prints both as algorithmic
 GB/s over the same bytes, and K2's fraction of the pattern ceiling.  Output: one JSON line."""
 import json, os, sys
 import numpy as np, torch
@@ -29,6 +29,7 @@ def timed(fn, iters=30, rounds=5):
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 for w in (args[0].split(",") if args else ["c2", "c3", "c4", "c1"]):
     sid, n, stride, _ = WORKLOADS[w]
+    stride = next((int(a[9:]) for a in sys.argv if a.startswith("--stride=")), stride)   # e.g. c1 in 2-KB frames
     arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
     d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
     V.synth(arena, n, stride, 0, sid, 0x20241020, 0, d)
