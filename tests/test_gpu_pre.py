@@ -679,3 +679,68 @@ def test_service_grids_of_four_contexts_in_threads(V, orc):
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_service_one_context_two_threads(V, orc):
+    """Two threads sharing ONE context with its service grid on (the C-ABI is thread-safe: the
+    context's mutex orders the submissions): each thread flushes NAT'd frames from
+    pre-images and verifies them, on its own half of one registered umem, submitting and waiting on
+    its own tickets while the other's batches come and go.  A submission that finds the other
+    thread's batch still on the grid completes it first (its results go to that thread's buffers);
+    every result equals the oracle's (Java's bytes), and every batch the grid took is counted."""
+    import threading
+    rng = np.random.default_rng(95)
+    after, desc, pre, want, _ = nat_case(orc, rng, 800, O.SYNTH_C5, pad=14, stride=2048, mask=NAT_FIELDS)
+    arena = after.copy()
+    c = V.Context(0, max_arena=arena.nbytes, max_pkts=512)
+    c.register(arena)
+    c.set_service(5000)
+    live = desc["flags"] != 0
+    errors, posted = [], [0, 0]
+
+    def frames(i):
+        o, L = int(desc[i]["l3_off"]), int(desc[i]["l3_len"])
+        return slice(o, o + L)
+
+    def work(k):
+        try:
+            r = np.random.default_rng(200 + k)
+            mine = np.arange(k, len(desc), 2)                 # disjoint frames per thread
+            for it in range(40):
+                b = int(r.choice([1, 5, 32, 200, 400]))
+                idx = np.sort(r.choice(mine, b, replace=False))
+                for i in idx:
+                    arena[frames(i)] = after[frames(i)]
+                out = np.zeros(b, np.uint32)
+                st = np.zeros(b, np.uint8)
+                t = c.submit_pre(arena, np.ascontiguousarray(desc[idx]), np.ascontiguousarray(pre[idx]), out, st,
+                                 O.MODE_WRITE)
+                c.wait(t)
+                vd = np.ascontiguousarray(desc[idx])
+                vd["flags"] = O.F_IP | O.F_L4
+                vst = np.zeros(b, np.uint8)
+                c.wait(c.submit(arena, vd, None, vst, O.MODE_VERIFY))
+                posted[k] += 2
+                for j, i in enumerate(idx):
+                    if not live[i]:
+                        continue
+                    if st[j] != O.S_DONE or not np.array_equal(arena[frames(i)], want[frames(i)]):
+                        errors.append((k, it, int(i), "flush"))
+                        return
+                    if (vst[j] & (O.S_IP_OK | O.S_L4_OK)) != (O.S_IP_OK | O.S_L4_OK):
+                        errors.append((k, it, int(i), "verify", int(vst[j])))
+                        return
+        except Exception as e:   # reported by the main thread
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(2)]
+    try:
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        assert not any(t.is_alive() for t in ts), "a thread did not finish"
+        assert not errors, errors[:4]
+        assert c.stats()["service_batches"] == sum(posted) == 160
+    finally:
+        c.close()
