@@ -406,6 +406,41 @@ def main():
         evs[i + 1].record(stream)
     torch.cuda.synchronize()
     per_launch = [evs[i].elapsed_ms(evs[i + 1]) for i in range(args.steps)]
+    # The same K steps with two batches in flight: the launches alternate between the kernel's
+    # stream and a second one (each with its own out words), so that one launch's ramp and drain
+    # overlap its neighbour's -- the rate of a caller that keeps two batches in flight, as the
+    # device group and the host contexts do.  Reported next to `value`, not as it: the roofline
+    # prices a launch alone, and overlapped launches have no duration of their own.
+    pipe_wall, pipe_bytes = 0.0, 0.0
+    if not nat:
+        if n:
+            if nb >= 2:
+                pb = [(arenas[0], ds[0], batch_bytes[0]), (arenas[1], ds[1], batch_bytes[1])]
+            else:   # a second batch (the next disjoint sub-stream), so that no two launches share one
+                a2 = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+                d2 = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+                V.synth(a2, n, stride, 0, synth_id, SEED, first + world * n_cfg, d2, stream=stream)
+                pb = [(arena, d, bytes_per_step), (a2, d2, algorithmic_bytes(V.tensor_to_desc(d2)[:n]))]
+            s2 = torch.cuda.Stream()
+            out2 = torch.zeros_like(out)
+
+            def step2(i):
+                a, dd, _ = pb[i % 2]
+                V.compute(a, dd, n, (out, out2)[i % 2], None, V.MODE_COMPUTE, args.team, stream=(stream, s2)[i % 2])
+            for i in range(4):
+                step2(i)
+            pipe_bytes = float(sum(pb[i % 2][2] for i in range(args.steps)))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        if n:
+            for i in range(args.steps):
+                step2(i)
+        torch.cuda.synchronize()
+        pipe_wall = max_over_ranks(time.perf_counter() - t0)
+        pipe_bytes = sum_over_ranks(pipe_bytes)
+        pb = a2 = d2 = None
     wall_max = max_over_ranks(wall)
     # per-rank attribution of a multi-GPU line: every rank's kernel time and the card it ran on
     props = torch.cuda.get_device_properties(torch.cuda.current_device())
@@ -638,6 +673,13 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if not nat and pipe_wall > 0:
+            pv = pipe_bytes / pipe_wall / 1e9
+            line["pipelined_two_streams"] = {"value": round(pv, 2), "unit": "GB/s",
+                                             "ms_per_step": round(pipe_wall / args.steps * 1e3, 5),
+                                             "over_value": round(pv / value, 4),
+                                             "what": "the same K steps alternating two streams (two batches in "
+                                                     "flight); not `value`: the roofline prices one launch alone"}
         if nat:
             line["config"]["Mpps_rank0"] = round(n / kernel_ms / 1e3, 1) if n else 0
         print(json.dumps(line), flush=True)
