@@ -411,6 +411,7 @@ def main():
     # overlap its neighbour's -- the rate of a caller that keeps two batches in flight, as the
     # device group and the host contexts do.  Reported next to `value`, not as it: the roofline
     # prices a launch alone, and overlapped launches have no duration of their own.
+    peak_main = int(torch.cuda.max_memory_allocated())   # before the second batch below
     pipe_wall, pipe_bytes = 0.0, 0.0
     if not nat:
         if n:
@@ -449,7 +450,7 @@ def main():
                                     "kernel_ms": round(t_beg.elapsed_ms(t_end) / args.steps, 5),
                                     "packets": int(n), "first_packet": int(first),
                                     "shard_arena_bytes": int(n) * stride,
-                                    "peak_alloc_bytes": int(torch.cuda.max_memory_allocated())})
+                                    "peak_alloc_bytes": peak_main})
     # bytes of the K timed launches (the rotation's batches differ slightly in C3's mix)
     timed_bytes = sum(batch_bytes[i % nb] for i in range(args.steps)) if not nat else bytes_per_step * args.steps
     total_bytes_step = sum_over_ranks(float(timed_bytes)) / args.steps

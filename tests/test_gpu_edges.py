@@ -42,7 +42,7 @@ def packets():
 
 def _gpu(V, arena_np, desc_np, mode, team=0):
     import torch
-    arena = torch.from_numpy(arena_np.copy()).cuda()
+    arena = torch.from_numpy(arena_np.copy()).pin_memory().cuda()
     n = len(desc_np)
     out = torch.zeros(n, dtype=torch.int32, device="cuda")
     st = torch.zeros(n, dtype=torch.uint8, device="cuda")
@@ -223,9 +223,9 @@ def _force_nat_zero(arena, d, r):
 
 def _gpu_nat(V, arena_np, desc, rw, mode):
     import torch
-    arena = torch.from_numpy(arena_np.copy()).cuda()
+    arena = torch.from_numpy(arena_np.copy()).pin_memory().cuda()
     st = torch.zeros(len(desc), dtype=torch.uint8, device="cuda")
-    V.nat4(arena, V.desc_to_tensor(desc), torch.from_numpy(rw.view(np.uint8).copy()).cuda(), len(desc), st, mode)
+    V.nat4(arena, V.desc_to_tensor(desc), torch.from_numpy(rw.view(np.uint8).copy()).pin_memory().cuda(), len(desc), st, mode)
     torch.cuda.synchronize()
     return arena.cpu().numpy(), st.cpu().numpy()
 

@@ -30,7 +30,7 @@ def V():
 
 def dev(a):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().cuda()
 
 
 def gpu_compute(V, arena_np, desc_np, mode=O.MODE_COMPUTE, team_log2=0, write=False):
@@ -603,7 +603,7 @@ def test_full_size_configs_equal_oracle(V, orc, cfg):
                       "c3": (O.SYNTH_C3, 1 << 20, 2048), "c4": (O.SYNTH_C4, 1 << 18, 9216)}[cfg]
     a, d = orc.synth(n, stride, 0, sid, O.SEED, 0)
     want, want_st = orc.process(a, d, threads=8)
-    arena = torch.from_numpy(a).cuda()
+    arena = torch.from_numpy(a).pin_memory().cuda()
     dt = V.desc_to_tensor(d)
     del a
     out = torch.zeros(n, dtype=torch.int32, device="cuda")
@@ -1201,7 +1201,7 @@ def test_arena_beyond_4gib(V, orc, order):
     if order == "shuffled":
         rng.shuffle(bases)
     dg = d.copy()
-    src = torch.from_numpy(a).cuda()
+    src = torch.from_numpy(a).pin_memory().cuda()
     for i in range(n):
         big[int(bases[i]): int(bases[i]) + stride] = src[i * stride:(i + 1) * stride]
         dg[i]["l3_off"] = int(bases[i]) + int(d[i]["l3_off"]) - i * stride
@@ -1236,7 +1236,7 @@ def test_batches_straddling_4gib(V, orc):
         a, d = orc.synth(m, stride, pad, sid, O.SEED, 77)
         want, want_st = orc.process(a, d, O.MODE_COMPUTE)
         big = torch.zeros(base + len(a) + 4096, dtype=torch.uint8, device="cuda")
-        big[base:base + len(a)] = torch.from_numpy(a).cuda()
+        big[base:base + len(a)] = torch.from_numpy(a).pin_memory().cuda()
         dg = d.copy()
         dg["l3_off"] += base
         assert int(dg["l3_off"].min()) < (4 << 30) < int(dg["l3_off"].max())
@@ -1278,7 +1278,7 @@ def test_windowed_k2_past_4gib(V, orc, order):
     for k, (sid, m, stride, pad, base) in enumerate(pieces):
         a, d = orc.synth(m, stride, pad, sid, O.SEED, 1000 * k)
         w, _ = orc.process(a, d, O.MODE_COMPUTE)
-        big[base:base + len(a)] = torch.from_numpy(a).cuda()
+        big[base:base + len(a)] = torch.from_numpy(a).pin_memory().cuda()
         dg = d.copy()
         dg["l3_off"] += base
         arrs.append((base, a, d))
@@ -1416,7 +1416,7 @@ def test_nat_arena_beyond_4gib(V, orc):
     bases = np.sort(rng.choice(((5 << 30) - (1 << 20)) // 16384, n, replace=False)) * 16384 + 8
     bases[: n // 3] = np.arange(n // 3) * 16384 + 8
     dg = desc.copy()
-    src = torch.from_numpy(arena).cuda()
+    src = torch.from_numpy(arena).pin_memory().cuda()
     for i in range(n):
         big[int(bases[i]): int(bases[i]) + stride] = src[i * stride:(i + 1) * stride]
         dg[i]["l3_off"] = int(bases[i]) + int(desc[i]["l3_off"]) - i * stride

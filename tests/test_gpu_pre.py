@@ -36,7 +36,7 @@ def V():
 
 def dev(a):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).pin_memory().cuda()
 
 
 def pre_images(arena, desc, rw):

@@ -85,9 +85,9 @@ def test_gpu_tuples_equal_testpcap_table():
         arena += f
     arena = np.frombuffer(bytes(arena) + bytes(64), np.uint8).copy()
     n = len(frames)
-    ga = torch.from_numpy(arena).cuda()
-    go = torch.from_numpy(np.array(offs, np.uint64)).cuda()
-    gl = torch.from_numpy(np.array(lens, np.uint32)).cuda()
+    ga = torch.from_numpy(arena).pin_memory().cuda()
+    go = torch.from_numpy(np.array(offs, np.uint64)).pin_memory().cuda()
+    gl = torch.from_numpy(np.array(lens, np.uint32)).pin_memory().cuda()
     d = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
     st = torch.zeros(n, dtype=torch.uint8, device="cuda")
     tu = torch.full((n * V.TUPLE_DTYPE.itemsize,), 0xAB, dtype=torch.uint8, device="cuda")

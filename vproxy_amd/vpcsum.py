@@ -526,7 +526,10 @@ class Group:
 
 def desc_to_tensor(desc: np.ndarray, device="cuda"):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(desc).view(np.uint8).copy()).to(device)
+    t = torch.from_numpy(np.ascontiguousarray(desc).view(np.uint8).copy())
+    # through page-locked memory: no pageable host-to-device copy of an array whose addresses a
+    # context may have registered and unregistered before (DESIGN_HISTORY.md "Round 5: experiments")
+    return (t.pin_memory() if str(device).startswith("cuda") else t).to(device)
 
 
 def tensor_to_desc(t) -> np.ndarray:
