@@ -84,6 +84,8 @@ def test_bench_two_ranks_strong_shards_per_rank_with_cpu_baseline():
         assert rr["peak_alloc_bytes"] < 0.6 * global_arena, rr
     assert j["cpu_baseline"] and j["cpu_baseline"]["value"] > 0 and j["cpu_baseline"]["cores"] >= 1
     assert c["oracle_gate"]["oracle_equal"] is True and c["oracle_gate"]["sample_equal"] is True
+    # the two-stream pass ran on every rank (its second batch not counted in the peak above)
+    assert j["pipelined_two_streams"]["value"] > 0 and j["pipelined_two_streams"]["ms_per_step"] > 0
 
 
 def test_descriptor_only_synth_equals_full_synth():
