@@ -415,8 +415,8 @@ def main():
     pipe_wall, pipe_bytes = 0.0, 0.0
     if not nat:
         if n:
-            if nb >= 2:
-                pb = [(arenas[0], ds[0], batch_bytes[0]), (arenas[1], ds[1], batch_bytes[1])]
+            if nb >= 2:   # the rotation's batches, as in the timed region
+                pb = [(arenas[b], ds[b], batch_bytes[b]) for b in range(nb)]
             else:   # a second batch (the next disjoint sub-stream), so that no two launches share one
                 a2 = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
                 d2 = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
@@ -426,11 +426,11 @@ def main():
             out2 = torch.zeros_like(out)
 
             def step2(i):
-                a, dd, _ = pb[i % 2]
+                a, dd, _ = pb[i % len(pb)]
                 V.compute(a, dd, n, (out, out2)[i % 2], None, V.MODE_COMPUTE, args.team, stream=(stream, s2)[i % 2])
             for i in range(4):
                 step2(i)
-            pipe_bytes = float(sum(pb[i % 2][2] for i in range(args.steps)))
+            pipe_bytes = float(sum(pb[i % len(pb)][2] for i in range(args.steps)))
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
