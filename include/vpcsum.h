@@ -40,8 +40,12 @@ extern "C" {
  * 3 (round 5): VPCSUM_F_PRE and the pre-image entry points (vpcsum_pre_async,
  * vpcsum_ctx_submit_pre, vpcsum_group_submit_pre, vpcsum_batch_submit_pre, VPCsum.submitPre);
  * vpcsum_compute_async leaves F_PRE descriptors to vpcsum_pre_async; a handle of the process-wide
- * group from before a vpcsum_shutdown is refused. */
-#define VPCSUM_ABI_VERSION 3
+ * group from before a vpcsum_shutdown is refused.
+ * 4 (round 6): the ingress header sum (vpcsum_hsum_t, VPCSUM_PRE_HSUM entries;
+ * vpcsum_ctx_verify_frames_hsum, vpcsum_parse_ether_hsum_async, VPCsum.verifyFramesHsum): the
+ * egress pre-image flush no longer depends on which setters ran; vpcsum_ctx_submit stages memory
+ * the context has not registered instead of copying from it directly. */
+#define VPCSUM_ABI_VERSION 4
 
 /* ------------------------------------------------------------------------ */
 /* Data formats                                                             */
@@ -161,6 +165,35 @@ typedef vpcsum_nat4_t vpcsum_pre4_t;
 #define VPCSUM_PRE_FMT_PRE4 0u   /* vpcsum_pre4_t entries */
 #define VPCSUM_PRE_FMT_PRE  1u   /* vpcsum_pre_t entries  */
 
+/* Ingress header sum of a received TCP / UDP frame, recorded by the RX verify
+ * (vpcsum_ctx_verify_frames_hsum) from the frame as it arrived.  `sum` is the one's complement sum
+ * (16-bit big-endian words, folded end-around; host order) of every word of the L4 sum that the
+ * vswitch's in-place setters can reach: the pseudo-header addresses (IPv4 L3+12..19, IPv6
+ * L3+8..39) and the L4 header's words [0, hlen) except the checksum field -- ports, sequence and
+ * acknowledgement numbers, flags, window, options (TcpPacket.java:31-110, TcpOption.setData
+ * :561-569; UdpPacket.java:188-209; Ipv4Packet/Ipv6Packet.setSrc/setDst).  At egress
+ * (VPCSUM_PRE_HSUM) the L4 sum is updated from it, RFC 1624 eqn. 3 with the header as one word:
+ * HC' = ~(~HC + ~sum + sum'), sum' the same words of the frame now.  That equals Java's full
+ * recompute (getRawPacket(0), AbstractPacket.java:15-22) for ANY change of those words, provided the
+ * stored HC was correct on receipt (VPCSUM_S_L4_OK) and the payload and lengths are the received
+ * ones: the caller's part (INTEGRATION.md §5 gives the vswitch's rule).  l2_len = 0: no record
+ * (not TCP / UDP, a refused frame, a segment shorter than its header). */
+typedef struct vpcsum_hsum {
+    uint16_t sum;
+    uint16_t l4_len;   /* segment length on receipt: l3_len - l4_off                         */
+    uint8_t  hlen;     /* L4 header bytes summed: TCP data offset * 4 (20..60), UDP 8         */
+    uint8_t  l4_proto; /* 6 / 17                                                              */
+    uint8_t  l3_ver;   /* 4 / 6                                                               */
+    uint8_t  l2_len;   /* 14 / 18 (802.1Q): the L3 header's offset in the frame; 0: no record  */
+} vpcsum_hsum_t;       /* 8 bytes */
+
+/* vpcsum_pre_t / vpcsum_pre4_t mask bit: the entry's first 8 bytes (src[0..7], or src[0..3] and
+ * dst[0..3] of a vpcsum_pre4_t) hold the packet's vpcsum_hsum_t instead of old addresses and
+ * ports (the other mask bits are then ignored).  The packet is refused (S_BAD_DESC, nothing
+ * written) unless its version, protocol, segment length and L4 header length (the TCP data offset
+ * now in the frame) equal the record's. */
+#define VPCSUM_PRE_HSUM 0x80u
+
 /* ------------------------------------------------------------------------ */
 /* Library / device                                                         */
 /* ------------------------------------------------------------------------ */
@@ -241,6 +274,13 @@ int vpcsum_parse_ether_tuples_async(const uint8_t* d_arena, uint64_t arena_len,
                                     const uint64_t* d_frame_off, const uint32_t* d_frame_len, uint32_t n,
                                     uint8_t flags, vpcsum_desc_t* d_desc, uint8_t* d_status,
                                     vpcsum_tuple_t* d_tuples, void* stream);
+
+/* vpcsum_parse_ether_async that also writes each frame's ingress header sum (vpcsum_hsum_t,
+ * l2_len 0 for a frame without one) to d_hsum, from the header bytes the parse reads. */
+int vpcsum_parse_ether_hsum_async(const uint8_t* d_arena, uint64_t arena_len,
+                                  const uint64_t* d_frame_off, const uint32_t* d_frame_len, uint32_t n,
+                                  uint8_t flags, vpcsum_desc_t* d_desc, uint8_t* d_status,
+                                  vpcsum_hsum_t* d_hsum, void* stream);
 
 /* Streaming-read ceiling probe: reads `bytes` from d_buf with 16-B lanes, writes one word per
  * block into d_sink.  Used by bench.py to report a measured HBM read roof next to 8 TB/s. */
@@ -325,6 +365,12 @@ int vpcsum_ctx_stats(vpcsum_ctx_t* ctx, uint64_t* service_batches, uint64_t* ser
 int vpcsum_ctx_verify_frames(vpcsum_ctx_t* ctx, const uint8_t* h_arena, uint64_t arena_len,
                              const uint64_t* h_frame_off, const uint32_t* h_frame_len, uint32_t n,
                              uint32_t* h_out, uint8_t* h_status, uint64_t* ticket);
+/* vpcsum_ctx_verify_frames that also records every frame's ingress header sum in h_hsum (n
+ * vpcsum_hsum_t, valid at vpcsum_ctx_wait): what the egress flush of the frame needs for a
+ * VPCSUM_PRE_HSUM pre-image after the vswitch's in-place setters ran. */
+int vpcsum_ctx_verify_frames_hsum(vpcsum_ctx_t* ctx, const uint8_t* h_arena, uint64_t arena_len,
+                                  const uint64_t* h_frame_off, const uint32_t* h_frame_len, uint32_t n,
+                                  uint32_t* h_out, uint8_t* h_status, vpcsum_hsum_t* h_hsum, uint64_t* ticket);
 /* Batched parse of a received batch with flow tuples (the conntrack key TcpInput / UdpInput read,
  * TcpInput.java:47-51, UdpInput.java:45-47): the frames of a registered arena, as for
  * vpcsum_ctx_verify_frames, are parsed on the GPU where they lie; at vpcsum_ctx_wait h_desc[i]
@@ -469,6 +515,12 @@ int Java_io_vproxy_vpcsum_VPCsum_submit(PNIEnv_vpcsum_long* env, int64_t ctx, vo
  *                     MemorySegment frameLen, int n, MemorySegment out, MemorySegment status) -> long ticket */
 int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
                                               void* frameOff, void* frameLen, int32_t n, void* out, void* status);
+/* VPCsum.verifyFramesHsum(long ctx, MemorySegment arena, long arenaLen, MemorySegment frameOff,
+ *                         MemorySegment frameLen, int n, MemorySegment out, MemorySegment status,
+ *                         MemorySegment hsum) -> long ticket (vpcsum_ctx_verify_frames_hsum) */
+int Java_io_vproxy_vpcsum_VPCsum_verifyFramesHsum(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                                  void* frameOff, void* frameLen, int32_t n, void* out, void* status,
+                                                  void* hsum);
 /* VPCsum.parseFrames(long ctx, MemorySegment arena, long arenaLen, MemorySegment frameOff,
  *                    MemorySegment frameLen, int n, MemorySegment desc, MemorySegment status,
  *                    MemorySegment tuples) -> long ticket */

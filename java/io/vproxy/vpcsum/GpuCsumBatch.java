@@ -39,11 +39,13 @@ import java.lang.foreign.ValueLayout;
  * verify overwrites it).  Copy what must outlive that, or pass your own segment to the overloads
  * that take one.
  *
- * NAT'd frames (INTEGRATION.md §5): {@link PreImage#record} in SwitchUtils.applyNat keeps the old
- * addresses / ports before the setters; {@link #defer} then marks the frame F_PRE when the ingress
- * verify proved its stored L4 sum (PacketBuffer.csumStatus has S_L4_OK), and the flush updates its
- * L4 sum from the pre-image reading only the header (VPCsum.submitPre).  Without that proof the
- * frame is summed in full, like Java's getRawPacket(0).
+ * Received frames changed in place (INTEGRATION.md §5): {@link #verifyFrames} records each frame's
+ * ingress header sum with its status ({@link PreImage#received}); {@link #defer} marks a frame F_PRE
+ * when {@link PreImage#eligible} holds -- verified L4 sum, the received frame leaving in place, the
+ * record's lengths -- and the flush updates its L4 sum from the record and the header words now in
+ * the frame, whatever the setters changed there (NAT, the PROXY-protocol SYN rewrite, an MSS clamp),
+ * reading only the header (VPCsum.submitPre).  Otherwise the frame is summed in full, like Java's
+ * getRawPacket(0).
  *
  * {@link #stats} counts where every deferred frame went (GPU, small-flush hand-back, rejected
  * descriptor hand-back), next to IfaceStatistics: with INTEGRATION.md §3's diff the interface keeps
@@ -59,6 +61,7 @@ public final class GpuCsumBatch implements AutoCloseable {
     private final Arena arena = Arena.ofShared();
     private final MemorySegment desc;
     private final MemorySegment pre;      // pre-images of the F_PRE frames (48 B per descriptor slot)
+    private final MemorySegment hsum;     // ingress header sums of the last verified RX batch (8 B per frame)
     private int nPre = 0;                 // F_PRE frames in the pending descriptor batch
     private final MemorySegment out;
     private final MemorySegment status;
@@ -82,8 +85,9 @@ public final class GpuCsumBatch implements AutoCloseable {
         public long smallFlushHandedBack;  // frames of flushes below SMALL_FLUSH, back to vpxdp
         public long badDescHandedBack;     // frames the kernel refused (S_BAD_DESC), back to vpxdp
         public long gpuFlushes;            // flushes that went to the GPU
-        public long preDeferred;           // NAT'd frames updated from their pre-image (F_PRE, header only)
-        public long preFull;               // NAT'd frames without a verified L4 sum: full recompute
+        public long preDeferred;           // received frames updated from their header sum (F_PRE, header only)
+        public long preFull;               // received frames with a record that took the full recompute
+                                           // (no verified L4 sum, rebuilt, moved, other lengths)
 
         @Override
         public String toString() {
@@ -119,6 +123,7 @@ public final class GpuCsumBatch implements AutoCloseable {
         VPCsum.get().setService(env, ctx, 20_000);
         this.desc = arena.allocate((long) DESC * capacity, 16);
         this.pre = arena.allocate((long) VPCsum.PRE_ENTRY * capacity, 16);
+        this.hsum = arena.allocate((long) VPCsum.HSUM_ENTRY * capacity, 16);
         this.out = arena.allocate(4L * capacity, 16);
         this.status = arena.allocate(capacity, 16);
         this.chunks = new ChunkInfo[capacity];
@@ -205,19 +210,6 @@ public final class GpuCsumBatch implements AutoCloseable {
         if (n == capacity) {
             throw new IllegalStateException("batch full: flush first");
         }
-        // a NAT'd frame (PreImage.record ran in SwitchUtils.applyNat) whose stored L4 sum the
-        // ingress verify proved: its L4 sum is updated from the pre-image, only its header read
-        PreImage pi = pkb.csumPre;
-        if ((flags & VPCsum.F_L4) != 0 && pi != null && pi.isValid()) {
-            if (pkb.csumStatus >= 0 && (pkb.csumStatus & (VPCsum.S_L4_OK | VPCsum.S_BAD_DESC)) == VPCsum.S_L4_OK) {
-                flags |= VPCsum.F_PRE;
-                pi.writeTo(pre, (long) VPCsum.PRE_ENTRY * n);
-                ++nPre;
-                ++stats.preDeferred;
-            } else {
-                ++stats.preFull;
-            }
-        }
         long l3 = frameAddr + (((EthernetPacket) pkb.pkt).getVlan() >= 0 ? 18 : 14);
         // The lengths come from the IP header fields, never from the buffer: a frame parsed with
         // allowPartial (every XDP / tap frame, PacketBuffer.java:177 -> EthernetPacket.java:52-56)
@@ -235,11 +227,24 @@ public final class GpuCsumBatch implements AutoCloseable {
             l3len = 40 + v6.getPayloadLength();    // Ipv6Packet.java:332
             l4off = v6.getHeaderSize();            // :427-435, extHeaders filled by from() (:33-35)
         }
+        int ver = ip instanceof Ipv4Packet ? 4 : 6;
+        // a received frame changed in place whose stored L4 sum the ingress verify proved: its L4
+        // sum is updated from its ingress header sum, only its header read (PreImage)
+        if ((flags & VPCsum.F_L4) != 0 && pkb.csumHsum != 0) {
+            if (PreImage.eligible(pkb, chunk, umem, l3, ver, ip.getProtocol(), l3len, l4off)) {
+                flags |= VPCsum.F_PRE;
+                PreImage.writeTo(pre, (long) VPCsum.PRE_ENTRY * n, pkb.csumHsum);
+                ++nPre;
+                ++stats.preDeferred;
+            } else {
+                ++stats.preFull;
+            }
+        }
         long d = (long) DESC * n;
         desc.set(ValueLayout.JAVA_LONG_UNALIGNED, d, l3);
         desc.set(ValueLayout.JAVA_SHORT_UNALIGNED, d + 8, (short) l3len);
         desc.set(ValueLayout.JAVA_SHORT_UNALIGNED, d + 10, (short) l4off);
-        desc.set(ValueLayout.JAVA_BYTE, d + 12, (byte) (ip instanceof Ipv4Packet ? 4 : 6));
+        desc.set(ValueLayout.JAVA_BYTE, d + 12, (byte) ver);
         desc.set(ValueLayout.JAVA_BYTE, d + 13, (byte) ip.getProtocol());
         desc.set(ValueLayout.JAVA_BYTE, d + 14, (byte) flags);
         desc.set(ValueLayout.JAVA_BYTE, d + 15, (byte) 0);
@@ -365,21 +370,31 @@ public final class GpuCsumBatch implements AutoCloseable {
      * Ingress verify straight from the RX ring (XDPIface.readable, XDPIface.java:281-314): the
      * {@code count} received frames at umem offsets {@code frameOff} (u64 each) with lengths
      * {@code frameLen} (u32 each) are parsed and verified on the GPU in one submission, without
-     * building descriptors in Java.  Returns one status byte per frame, in this instance's
-     * segment, valid until the next call on it (see the class note).
+     * building descriptors in Java, and each frame's ingress header sum is recorded
+     * ({@link #headerSums}).  Returns one status byte per frame, in this instance's segment, valid
+     * until the next call on it (see the class note).  Hand both to each frame's PacketBuffer with
+     * {@link PreImage#received}.
      */
     public MemorySegment verifyFrames(MemorySegment frameOff, MemorySegment frameLen, int count) throws IOException {
-        return verifyFrames(frameOff, frameLen, count, status);
+        return verifyFrames(frameOff, frameLen, count, status, hsum);
     }
 
-    /** {@link #verifyFrames} with the status bytes written to the caller's {@code statusOut}. */
+    /** {@link #verifyFrames} with the status bytes and header sums (8 B per frame) written to the
+     * caller's segments. */
     public MemorySegment verifyFrames(MemorySegment frameOff, MemorySegment frameLen, int count,
-                                      MemorySegment statusOut) throws IOException {
+                                      MemorySegment statusOut, MemorySegment hsumOut) throws IOException {
         // no out words: the status bytes are the ingress result (writing the sums too cost verify 4%
         // on 64-B frames, DESIGN.md §5)
-        long t = VPCsum.get().verifyFrames(env, ctx, umem, umemLen, frameOff, frameLen, count, MemorySegment.NULL, statusOut);
+        long t = VPCsum.get().verifyFramesHsum(env, ctx, umem, umemLen, frameOff, frameLen, count, MemorySegment.NULL,
+                                               statusOut, hsumOut);
         VPCsum.get().waitFor(env, ctx, t);
         return statusOut;
+    }
+
+    /** The header sums of the last {@link #verifyFrames} batch (8 B per frame), valid until the next
+     * verify on this instance. */
+    public MemorySegment headerSums() {
+        return hsum;
     }
 
     /**

@@ -35,10 +35,10 @@ public class VPCsum {
         return INSTANCE;
     }
 
-    /** include/vpcsum.h VPCSUM_ABI_VERSION this binding was written against (3: VPCSUM_F_PRE and
-     * submitPre; 2: NAT_DEC_TTL refuses TTL <= 1 with S_TTL_EXPIRED).  {@link #abiVersion} reports
-     * the loaded library's. */
-    public static final int ABI_VERSION = 3;
+    /** include/vpcsum.h VPCSUM_ABI_VERSION this binding was written against (4: the ingress header
+     * sum, verifyFramesHsum and PRE_HSUM entries; 3: VPCSUM_F_PRE and submitPre; 2: NAT_DEC_TTL
+     * refuses TTL <= 1 with S_TTL_EXPIRED).  {@link #abiVersion} reports the loaded library's. */
+    public static final int ABI_VERSION = 4;
 
     /** vpcsum_abi_version() of the loaded library (a plain C function, no PNIEnv; {@link VPCsumLib}).
      * Throws an IOException when libvpcsum is not loaded. */
@@ -52,11 +52,16 @@ public class VPCsum {
     public static final int F_RAW = 0x04;
     /** checksum offload (VP_CSUM_UP_PSEUDO): L4 field = folded pseudo-header sum (CHECKSUM_PARTIAL) */
     public static final int F_L4P = 0x08;
-    /** NAT'd packet whose stored L4 sum was verified on ingress: its L4 sum is updated from its
-     * pre-image (the old addresses / ports, {@link PreImage}) by RFC 1624 -- only the header is read */
+    /** a received packet changed in place whose stored L4 sum was verified on ingress: its L4 sum
+     * is updated from its pre-image entry by RFC 1624 -- only the header is read ({@link PreImage}) */
     public static final int F_PRE = 0x10;
-    /** bytes of one vpcsum_pre_t pre-image entry (the vpcsum_nat_t layout, old values) */
+    /** bytes of one vpcsum_pre_t pre-image entry (the vpcsum_nat_t layout) */
     public static final int PRE_ENTRY = 48;
+    /** pre-image entry mask: the entry's first 8 bytes hold the frame's ingress header sum
+     * (vpcsum_hsum_t, {@link #verifyFramesHsum}) */
+    public static final int PRE_HSUM = 0x80;
+    /** bytes of one vpcsum_hsum_t: sum(u16) l4Len(u16) hlen proto ver l2Len */
+    public static final int HSUM_ENTRY = 8;
     // status bits
     public static final int S_IP_OK = 0x01;
     public static final int S_L4_OK = 0x02;
@@ -149,10 +154,11 @@ public class VPCsum {
         long.class /* arenaLen */, MemorySegment.class /* desc */, MemorySegment.class /* pre */, int.class /* n */,
         MemorySegment.class /* out */, MemorySegment.class /* status */, int.class /* mode */);
 
-    /** {@link #submit} for an egress batch that holds NAT'd frames: descriptors with F_PRE take their
-     * L4 sum from {@code pre[i]} (48-B vpcsum_pre_t, {@link PreImage#writeTo}) by RFC 1624, reading
-     * only the frame's header; the others are summed in full (vpcsum_ctx_submit_pre).  mode:
-     * MODE_COMPUTE or MODE_WRITE.  Returns a ticket for {@link #waitFor}. */
+    /** {@link #submit} for an egress batch that holds frames changed in place: descriptors with
+     * F_PRE take their L4 sum from {@code pre[i]} (48-B vpcsum_pre_t: a PRE_HSUM entry,
+     * {@link PreImage#writeTo}) by RFC 1624, reading only the frame's header; the others are summed
+     * in full (vpcsum_ctx_submit_pre).  mode: MODE_COMPUTE or MODE_WRITE.  Returns a ticket for
+     * {@link #waitFor}. */
     public long submitPre(PNIEnv ENV, long ctx, MemorySegment arena, long arenaLen, MemorySegment desc, MemorySegment pre,
                           int n, MemorySegment out, MemorySegment status, int mode) throws java.io.IOException {
         ENV.reset();
@@ -204,6 +210,34 @@ public class VPCsum {
         int ERR;
         try {
             ERR = (int) verifyFramesMH.invokeExact(ENV.MEMORY, ctx, arena, arenaLen, frameOff, frameLen, n, out, status);
+        } catch (Throwable THROWABLE) {
+            throw PanamaUtils.convertInvokeExactException(THROWABLE);
+        }
+        if (ERR != 0) {
+            ENV.throwIf(java.io.IOException.class);
+            ENV.throwLast();
+        }
+        return ENV.returnLong();
+    }
+
+    private static final MethodHandle verifyFramesHsumMH = PanamaUtils.lookupPNIFunction(new PNILinkOptions().setCritical(false),
+        "Java_io_vproxy_vpcsum_VPCsum_verifyFramesHsum", long.class /* ctx */, MemorySegment.class /* arena */,
+        long.class /* arenaLen */, MemorySegment.class /* frameOff */, MemorySegment.class /* frameLen */, int.class /* n */,
+        MemorySegment.class /* out */, MemorySegment.class /* status */, MemorySegment.class /* hsum */);
+
+    /** {@link #verifyFrames} that also records each frame's ingress header sum: hsum[i] (8 B,
+     * vpcsum_hsum_t: the sum of the L4 sum's words the in-place setters can reach, the segment and
+     * header lengths, protocol, version and the L3 offset in the frame; all zero for a frame without
+     * one).  The egress flush of a frame changed in place updates its L4 sum from it
+     * ({@link GpuCsumBatch#defer}, INTEGRATION.md §5).  Returns a ticket for {@link #waitFor}. */
+    public long verifyFramesHsum(PNIEnv ENV, long ctx, MemorySegment arena, long arenaLen, MemorySegment frameOff,
+                                 MemorySegment frameLen, int n, MemorySegment out, MemorySegment status,
+                                 MemorySegment hsum) throws java.io.IOException {
+        ENV.reset();
+        int ERR;
+        try {
+            ERR = (int) verifyFramesHsumMH.invokeExact(ENV.MEMORY, ctx, arena, arenaLen, frameOff, frameLen, n, out, status,
+                                                       hsum);
         } catch (Throwable THROWABLE) {
             throw PanamaUtils.convertInvokeExactException(THROWABLE);
         }

@@ -42,7 +42,12 @@ NAT4_DTYPE = np.dtype([("src", "u1", 4), ("dst", "u1", 4), ("sport", "u1", 2), (
                        ("mask", "u1"), ("rsv", "u1", 3)])
 NAT_DTYPE = np.dtype([("src", "u1", 16), ("dst", "u1", 16), ("sport", "u1", 2), ("dport", "u1", 2),
                       ("mask", "u1"), ("ttl", "u1"), ("rsv", "u1", 10)])
+# vpcsum_hsum_t: the ingress header sum of a received TCP / UDP frame (include/vpcsum.h)
+HSUM_DTYPE = np.dtype([("sum", "<u2"), ("l4_len", "<u2"), ("hlen", "u1"), ("l4_proto", "u1"), ("l3_ver", "u1"),
+                       ("l2_len", "u1")])
+PRE_HSUM = 0x80   # VPCSUM_PRE_HSUM: a pre-image entry holding a vpcsum_hsum_t
 assert DESC_DTYPE.itemsize == 16 and NAT4_DTYPE.itemsize == 16 and NAT_DTYPE.itemsize == 48
+assert HSUM_DTYPE.itemsize == 8
 
 # Consts.java:24-31
 IP_PROTOCOL_ICMP, IP_PROTOCOL_TCP, IP_PROTOCOL_UDP, IP_PROTOCOL_ICMPv6 = 1, 6, 17, 58
@@ -393,6 +398,49 @@ def flow_tuple(frame: bytes) -> dict:
         if info.proto == IP_PROTOCOL_TCP:
             t["tcp_flags"] = _u16(l4, 12) & 0x3F
     return t
+
+
+def hdr_words(l3: bytes, ver: int, l4_off: int, hlen: int, proto: int) -> bytes:
+    """The words of the L4 sum an in-place setter of the vswitch can reach, as one byte string:
+    the pseudo-header addresses (Utils.buildPseudoIPv4Header / IPv6Header, Utils.java:758-776) and
+    the L4 header [0, hlen) with its checksum field as zeros -- TcpPacket.setSrcPort / setDstPort /
+    setSeqNum / setAckNum / setFlags and TcpOption.setData (TcpPacket.java:31-110, 561-569),
+    UdpPacket.setSrcPort / setDstPort (UdpPacket.java:188-209), Ipv4Packet / Ipv6Packet.setSrc /
+    setDst (Ipv4Packet.java:433-458, Ipv6Packet.java:374-396) all write inside it."""
+    addr = bytes(l3[12:20]) if ver == 4 else bytes(l3[8:40])
+    h = bytearray(l3[l4_off:l4_off + hlen])
+    f = L4_FIELD[proto]
+    h[f:f + 2] = b"\x00\x00"
+    return addr + bytes(h)
+
+
+def hsum_record(frame: bytes) -> np.void:
+    """The ingress header sum (vpcsum_hsum_t) of one received Ethernet frame, as the RX verify
+    records it: the frame parsed with the vswitch's rules (parse_ether); for TCP (data offset 20..
+    segment length) and UDP (8-B header in the segment) the per-step Java fold
+    (Utils.calculateChecksumIntermediate, Utils.java:783-797) of :func:`hdr_words`, the segment length,
+    the header length, protocol, version and the L3 header's offset in the frame; all zeros for
+    any other frame."""
+    r = np.zeros(1, HSUM_DTYPE)[0]
+    info, _ = parse_ether(frame)
+    if info is None or info.proto not in (IP_PROTOCOL_TCP, IP_PROTOCOL_UDP):
+        return r
+    l3 = bytes(frame)[info.l3_off:info.l3_off + info.l3_len]
+    seg = info.l3_len - info.l4_off
+    if info.proto == IP_PROTOCOL_TCP:
+        if seg < 20:
+            return r
+        hlen = (l3[info.l4_off + 12] >> 4) * 4
+        if hlen < 20 or hlen > seg:
+            return r
+    else:
+        if seg < 8:
+            return r
+        hlen = 8
+    w = hdr_words(l3, info.ver, info.l4_off, hlen, info.proto)
+    r["sum"] = csum_intermediate(0, w, len(w))
+    r["l4_len"], r["hlen"], r["l4_proto"], r["l3_ver"], r["l2_len"] = seg, hlen, info.proto, info.ver, info.l3_off
+    return r
 
 
 def pseudo_partial(l3: bytes, info: L3Info) -> int:

@@ -45,7 +45,7 @@ def test_so_loads_and_reports_abi(libpath):
     for f in header_functions():
         assert hasattr(L, f)
     L.vpcsum_abi_version.restype = ctypes.c_int
-    assert L.vpcsum_abi_version() == 3
+    assert L.vpcsum_abi_version() == 4
 
 
 def test_code_object_is_gfx950(libpath):

@@ -124,6 +124,8 @@ struct Slot {
     vpcsum_nat_t* d_rw = nullptr;
     vpcsum_tuple_t* h_tu = nullptr;    // flow tuples of a parse batch: pinned (mapped), allocated
     vpcsum_tuple_t* dh_tu = nullptr;   // with the context's first parse batch
+    vpcsum_hsum_t* h_hs = nullptr;     // ingress header sums of a verify batch: pinned (mapped),
+    vpcsum_hsum_t* dh_hs = nullptr;    // allocated with the context's first such batch
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     int kind = 0;                      // current batch: 0 checksums, 1 NAT rewrite, 2 parse
@@ -140,6 +142,7 @@ struct Slot {
     uint8_t* user_status = nullptr;
     vpcsum_desc_t* user_desc_out = nullptr;   // parse batch: where descriptors and tuples go
     vpcsum_tuple_t* user_tuples = nullptr;
+    vpcsum_hsum_t* user_hsum = nullptr;       // verify batch with header sums: where they go
 };
 
 }  // namespace vpcsum
@@ -148,8 +151,81 @@ struct Registered {
     uint8_t* host;
     uint64_t len;
     uint8_t* dev;    // device-side address of the page-locked mapping (zero-copy access)
-    bool owned;      // this context page-locked it (a group's contexts share one registration)
+    uint8_t* key;    // the process-wide page-lock this entry holds a reference on (hostlock_acquire);
+                     // nullptr: a mapping of its group's lock (the group holds the reference)
 };
+
+// ------------------------------------------------------------------------------------------
+// Process-wide registry of the host ranges libvpcsum page-locks.  HIP keys a host registration by
+// its start address (tools/reg_probe.py, profiles/r06c_reg_probe.jsonl): a second hipHostRegister
+// of a registered start -- same length or longer -- returns success without mapping anything new,
+// the first hipHostUnregister then drops the registration for both holders, and the second fails.
+// Two contexts (or a context and a group) registering one umem therefore left the survivor with a
+// mapping HIP had torn down, and its zero-copy kernels -- or a later pageable copy HIP resolves
+// through the orphaned registration -- reading unmapped memory (DESIGN_HISTORY.md "Round 6: the
+// intermittent fault").  So every page-lock goes through here: a range inside a live lock shares
+// it (reference counted), a range that partially overlaps one or that HIP already holds as
+// page-locked memory of another owner is refused, and hipHostUnregister runs once, with the last
+// reference.  Locks are mapped on every device (portable), so a share across devices is valid.
+// ------------------------------------------------------------------------------------------
+struct HostLock {
+    uint8_t* host;
+    uint64_t len;
+    uint32_t refs;
+};
+static std::mutex g_lock_mu;
+static std::vector<HostLock> g_locks;
+
+static bool hip_holds_pinned(const uint8_t* p) {
+    hipPointerAttribute_t a;
+    const bool pinned = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+    (void)hipGetLastError();   // an unknown (pageable) pointer leaves an error behind
+    return pinned;
+}
+
+using vpcsum::fail;
+using vpcsum::hipfail;
+
+// A reference on the page-lock of [p, p+len) (see HostLock): *key = the lock's start, for
+// hostlock_release.  Caller is on the device the mapping is wanted for.
+static int hostlock_acquire(uint8_t* p, uint64_t len, uint8_t** key, const char* what) {
+    std::lock_guard<std::mutex> lk(g_lock_mu);
+    for (auto& h : g_locks) {
+        if (p >= h.host && p + len <= h.host + h.len) {   // inside a live lock: share it
+            ++h.refs;
+            *key = h.host;
+            return 0;
+        }
+        if (p < h.host + h.len && h.host < p + len)
+            return fail("%s: [%p, +%llu) overlaps the arena [%p, +%llu) page-locked earlier: register one range "
+                        "that covers both",
+                        what, (void*)p, (unsigned long long)len, (void*)h.host, (unsigned long long)h.len);
+    }
+    if (hip_holds_pinned(p) || hip_holds_pinned(p + len - 1))
+        return fail("%s: %p is already page-locked outside libvpcsum (hipHostMalloc / hipHostRegister): its owner "
+                    "controls that lock's lifetime; pass the memory unregistered (staged) instead",
+                    what, (void*)p);
+    g_locks.reserve(g_locks.size() + 1);   // may throw: before anything is pinned
+    VPC_CHECK(hipHostRegister(p, len, hipHostRegisterMapped | hipHostRegisterPortable), "hipHostRegister");
+    g_locks.push_back({p, len, 1});
+    *key = p;
+    return 0;
+}
+
+// Drop one reference; the last one unpins (a failure is reported: the caller must not free the
+// memory as if it were unpinned).
+static int hostlock_release(uint8_t* key, const char* what) {
+    std::lock_guard<std::mutex> lk(g_lock_mu);
+    for (size_t i = 0; i < g_locks.size(); ++i) {
+        if (g_locks[i].host != key) continue;
+        if (--g_locks[i].refs) return 0;
+        g_locks.erase(g_locks.begin() + i);
+        const hipError_t e = hipHostUnregister(key);
+        if (e != hipSuccess) return fail("%s: hipHostUnregister(%p): %s", what, (void*)key, hipGetErrorString(e));
+        return 0;
+    }
+    return fail("%s: %p holds no page-lock of libvpcsum", what, (void*)key);
+}
 
 // Zero-copy batches (frames read over PCIe) of at most this many packets run one wave per packet.
 constexpr uint32_t kZeroCopyWaveTeams = 4096;
@@ -382,6 +458,21 @@ int vpcsum_parse_ether_tuples_async(const uint8_t* d_arena, uint64_t arena_len, 
     } VPC_CATCH("vpcsum_parse_ether_tuples_async")
 }
 
+int vpcsum_parse_ether_hsum_async(const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_frame_off,
+                                  const uint32_t* d_frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* d_desc,
+                                  uint8_t* d_status, vpcsum_hsum_t* d_hsum, void* stream) {
+    try {
+        if (n == 0) return 0;
+        if (!d_arena || !d_frame_off || !d_frame_len || !d_desc || !d_hsum)
+            return fail("vpcsum_parse_ether_hsum_async: NULL argument");
+        if ((uintptr_t)d_hsum & 7) return fail("vpcsum_parse_ether_hsum_async: header sums not 8-byte aligned");
+        VPC_CHECK(launch_parse_ether(d_arena, arena_len, d_frame_off, d_frame_len, n, flags, d_desc, d_status, nullptr,
+                                     (hipStream_t)stream, nullptr, d_hsum),
+                  "parse launch");
+        return 0;
+    } VPC_CATCH("vpcsum_parse_ether_hsum_async")
+}
+
 int vpcsum_read_probe_async(const uint8_t* d_buf, uint64_t bytes, uint32_t* d_sink, uint32_t grid, void* stream) {
     try {
         if (!d_buf || !d_sink) return fail("vpcsum_read_probe_async: NULL argument");
@@ -472,6 +563,7 @@ static void slot_free(Slot& s) {
     if (s.h_rw) (void)hipHostFree(s.h_rw);
     if (s.d_rw) (void)hipFree(s.d_rw);
     if (s.h_tu) (void)hipHostFree(s.h_tu);
+    if (s.h_hs) (void)hipHostFree(s.h_hs);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot();
@@ -603,8 +695,11 @@ int vpcsum_ctx_destroy(vpcsum_ctx_t* c) {
                 if (s.stream) (void)hipStreamSynchronize(s.stream);
                 slot_free(s);
             }
+            // every page-lock reference this context holds goes, each failure reported (the caller
+            // may free the arena once this returns: a range HIP still held as registered would be taken
+            // for pinned memory by a later copy from whatever is allocated there)
             for (auto& r : c->registered)
-                if (r.owned) (void)hipHostUnregister(r.host);
+                if (r.key && hostlock_release(r.key, "vpcsum_ctx_destroy") != 0) rc = -1;
         }
         delete c;
         return rc;
@@ -616,15 +711,18 @@ int vpcsum_ctx_register_arena(vpcsum_ctx_t* c, void* h_arena, uint64_t len) {
         if (!c || !h_arena || len == 0) return fail("vpcsum_ctx_register_arena: bad argument");
         std::lock_guard<std::mutex> lk(c->mu);
         VPC_ON_DEVICE(c->device);
+        for (auto& r : c->registered)
+            if (r.host == (uint8_t*)h_arena) return fail("vpcsum_ctx_register_arena: %p is registered already", h_arena);
         c->registered.reserve(c->registered.size() + 1);   // may throw: before anything is pinned
-        VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterMapped), "hipHostRegister");
+        uint8_t* key = nullptr;
+        if (hostlock_acquire((uint8_t*)h_arena, len, &key, "vpcsum_ctx_register_arena") != 0) return -1;
         void* dev = nullptr;
         hipError_t e = hipHostGetDevicePointer(&dev, h_arena, 0);
         if (e != hipSuccess) {
-            (void)hipHostUnregister(h_arena);
+            (void)hostlock_release(key, "vpcsum_ctx_register_arena");
             return hipfail(e, "hipHostGetDevicePointer");
         }
-        c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, true});
+        c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, key});
         return 0;
     } VPC_CATCH("vpcsum_ctx_register_arena")
 }
@@ -648,9 +746,9 @@ int vpcsum_ctx_unregister_arena(vpcsum_ctx_t* c, void* h_arena) {
         for (size_t i = 0; i < c->registered.size(); ++i) {
             if (c->registered[i].host == (uint8_t*)h_arena) {
                 if (ctx_quiesce_zero_copy(c) != 0) return -1;
-                if (c->registered[i].owned) VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
+                uint8_t* key = c->registered[i].key;
                 c->registered.erase(c->registered.begin() + i);
-                return 0;
+                return key ? hostlock_release(key, "vpcsum_ctx_unregister_arena") : 0;
             }
         }
         return fail("vpcsum_ctx_unregister_arena: arena not registered");
@@ -664,17 +762,13 @@ static uint8_t* mapped_dev(vpcsum_ctx* c, const uint8_t* p, uint64_t len) {
     return nullptr;
 }
 
-static bool is_registered(vpcsum_ctx* c, const uint8_t* p, uint64_t len) {
-    if (mapped_dev(c, p, len)) return true;
-    // page-locked elsewhere (hipHostMalloc, another library's hipHostRegister)?
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost) {
-        hipPointerAttribute_t b;
-        if (hipPointerGetAttributes(&b, p + len - 1) == hipSuccess && b.type == hipMemoryTypeHost) return true;
-    }
-    (void)hipGetLastError();
-    return false;
-}
+// Whether the staged path may DMA straight from [p, p+len): only when this context registered it
+// (its own registration or its group's), so the page-lock outlives the copy -- vpcsum_ctx_unregister
+// and destroy finish the context's batches before they unpin.  Memory page-locked by anyone else
+// (another context, hipHostMalloc, another library) is copied through the pinned staging first: its
+// owner may unpin or free it while the copy is in flight, which the library cannot see (round 5's
+// version trusted hipPointerGetAttributes here; DESIGN_HISTORY.md "Round 6: the intermittent fault").
+static bool is_registered(vpcsum_ctx* c, const uint8_t* p, uint64_t len) { return mapped_dev(c, p, len) != nullptr; }
 
 static uint32_t svc_done(const Service& v) { return __atomic_load_n(&v.mb->done, __ATOMIC_ACQUIRE); }
 
@@ -780,6 +874,9 @@ static int slot_finish(vpcsum_ctx* c, Slot& s) {
     const uint8_t* res_status = s.svc_seq ? c->svc.h_status : s.h_status;
     if (s.user_out) memcpy(s.user_out, res_out, (size_t)s.n * 4);
     if (s.user_status) memcpy(s.user_status, res_status, s.n);
+    if (s.user_hsum)   // a verify batch's header sums: the service's aux buffer, or the slot's staging
+        memcpy(s.user_hsum, s.svc_seq ? (const void*)c->svc.h_pre : (const void*)s.h_hs, (size_t)s.n * sizeof(vpcsum_hsum_t));
+    s.user_hsum = nullptr;
     if ((s.mode & VPCSUM_MODE_WRITE) && s.user_arena && !s.zero_copy) {
         // place the GPU results into the caller's frames (big endian, as ByteArray.int16)
         for (uint32_t i = 0; i < s.n; ++i) {
@@ -853,11 +950,12 @@ static int svc_quiesce(vpcsum_ctx* c) {
 // the frames are parsed only (vpcsum_ctx_parse_frames).
 static int svc_post(vpcsum_ctx* c, Slot& s, uint64_t t, uint8_t* h_arena, uint64_t arena_len, uint8_t* base,
                     const vpcsum_desc_t* h_desc, uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode,
-                    const void* h_pre, uint32_t pre_fmt, uint64_t* ticket, bool frames = false, bool parse = false) {
+                    const void* h_pre, uint32_t pre_fmt, uint64_t* ticket, bool frames = false, bool parse = false,
+                    bool hsum = false) {
     Service& v = c->svc;
     SvcMailbox* mb = v.mb;
     if (!frames) memcpy(v.h_desc, h_desc, (size_t)n * sizeof(vpcsum_desc_t));
-    uint64_t cmd = (frames ? kSvcFrames : 0) | (parse ? kSvcParse : 0);
+    uint64_t cmd = (frames ? kSvcFrames : 0) | (parse ? kSvcParse : 0) | (hsum ? kSvcHsum : 0);
     if (h_pre) {
         // the pre-images, each F_PRE frame's stored L4 sum copied into its entry's spare bytes
         // (vpcsum_pre4_t rsv[1..2], vpcsum_pre_t rsv[0..1]): the kernel takes the sum from there,
@@ -931,7 +1029,8 @@ static int svc_post(vpcsum_ctx* c, Slot& s, uint64_t t, uint8_t* h_arena, uint64
 // slot_finish hands them over; the frames themselves are written in place through the mapping.
 static int svc_post_frames(vpcsum_ctx* c, Slot& s, uint64_t t, const uint8_t* h_arena, uint64_t arena_len, uint8_t* base,
                            const uint64_t* h_off, const uint32_t* h_len, const uint8_t* h_flags, uint8_t flags,
-                           uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode, bool parse, uint64_t* ticket) {
+                           uint32_t n, uint32_t* h_out, uint8_t* h_status, uint32_t mode, bool parse, uint64_t* ticket,
+                           bool hsum = false) {
     if (svc_drain(c) != 0) return -1;
     SvcFrameRec* r = reinterpret_cast<SvcFrameRec*>(c->svc.h_desc);
     for (uint32_t i = 0; i < n; ++i) {
@@ -943,7 +1042,7 @@ static int svc_post_frames(vpcsum_ctx* c, Slot& s, uint64_t t, const uint8_t* h_
         memcpy(&r[i], &x, sizeof(x));
     }
     if (svc_post(c, s, t, const_cast<uint8_t*>(h_arena), arena_len, base, c->svc.h_desc, n, h_out, h_status, mode, nullptr,
-                 0, ticket, true, parse) != 0)
+                 0, ticket, true, parse, hsum) != 0)
         return -1;
     s.user_arena = nullptr;
     s.user_desc = nullptr;
@@ -1129,9 +1228,26 @@ int vpcsum_ctx_submit_pre(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len,
                 if ((d.flags & VPCSUM_F_PRE) && fld >= 0 && (uint32_t)d.l4_off + fld + 2u <= d.l3_len) {
                     const uint8_t* f = h_arena + d.l3_off + d.l4_off + fld;
                     if (!(d.l4_proto == 17 && f[0] == 0 && f[1] == 0)) {
-                        take = std::max<uint32_t>(d.l3_ver == 4 ? 20u : 40u, (uint32_t)d.l4_off + fld + 2u);
+                        // through the checksum field, or through the L4 header a header-sum entry covers
+                        const uint8_t* e = (const uint8_t*)h_pre + (size_t)i * esz;
+                        const uint8_t emask = e[pre_fmt == VPCSUM_PRE_FMT_PRE ? offsetof(vpcsum_pre_t, mask)
+                                                                               : offsetof(vpcsum_pre4_t, mask)];
+                        const uint32_t hl = (emask & VPCSUM_PRE_HSUM) ? e[offsetof(vpcsum_hsum_t, hlen)] : 0u;
+                        take = std::max<uint32_t>(d.l3_ver == 4 ? 20u : 40u,
+                                                  (uint32_t)d.l4_off + std::max<uint32_t>(fld + 2u, hl));
                         take = std::min<uint32_t>(take, d.l3_len);
                         s.h_desc[i].l3_len = (uint16_t)take;
+                        if (emask & VPCSUM_PRE_HSUM) {
+                            // the kernel checks the record's segment length against the descriptor's,
+                            // which is cut here: check it against the real one on the host, and hand the
+                            // kernel the cut length (or, on a mismatch, a record it refuses)
+                            vpcsum_hsum_t hs;
+                            uint8_t* se = (uint8_t*)s.h_rw + (size_t)i * esz;
+                            memcpy(&hs, se, sizeof(hs));
+                            if (hs.l4_len == (uint32_t)d.l3_len - d.l4_off) hs.l4_len = (uint16_t)(take - d.l4_off);
+                            else hs.l2_len = 0;
+                            memcpy(se, &hs, sizeof(hs));
+                        }
                     }
                 }
                 const uint64_t a0 = d.l3_off & ~(uint64_t)15;
@@ -1186,55 +1302,88 @@ int vpcsum_ctx_wait(vpcsum_ctx_t* c, uint64_t ticket) {
     } VPC_CATCH("vpcsum_ctx_wait")
 }
 
+// vpcsum_ctx_verify_frames / _hsum: h_hsum NULL = no header sums
+static int ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
+                             const uint32_t* h_frame_len, uint32_t n, uint32_t* h_out, uint8_t* h_status,
+                             vpcsum_hsum_t* h_hsum, uint64_t* ticket, const char* what) {
+    if (!c || !ticket) return fail("%s: NULL context or ticket", what);
+    if (n > c->max_pkts) return fail("%s: %u frames > capacity %u", what, n, c->max_pkts);
+    if (n && (!h_arena || !h_frame_off || !h_frame_len || !h_status))
+        return fail("%s: NULL arena, frame table or status", what);
+    std::lock_guard<std::mutex> lk(c->mu);
+    VPC_ON_DEVICE(c->device);
+    uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
+    if (n && !base) return fail("%s: the arena must be registered (vpcsum_ctx_register_arena)", what);
+    const uint64_t t = c->next_ticket++;
+    Slot& s = c->slots[t & 1];
+    if (s.busy && slot_finish(c, s) != 0) return -1;
+    if (h_hsum && n && !s.h_hs) {
+        hipError_t e = hipHostMalloc((void**)&s.h_hs, (size_t)c->max_pkts * sizeof(vpcsum_hsum_t),
+                                     hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s.dh_hs, s.h_hs, 0);
+        if (e != hipSuccess) {
+            if (s.h_hs) (void)hipHostFree(s.h_hs);
+            s.h_hs = s.dh_hs = nullptr;
+            return hipfail(e, what);
+        }
+    }
+    if (n && c->svc.on && n <= kSvcBatchMax) {
+        // a small received batch: the service grid parses and verifies each frame
+        // (kernels.hip svc_frame_packet), the sums into its own buffer (copied out only with h_out),
+        // the header sums into its aux buffer
+        if (svc_post_frames(c, s, t, h_arena, arena_len, base, h_frame_off, h_frame_len, nullptr, VPCSUM_F_IP | VPCSUM_F_L4,
+                            n, h_out, h_status, VPCSUM_MODE_VERIFY, false, ticket, h_hsum != nullptr) != 0)
+            return -1;
+        s.user_hsum = h_hsum;
+        return 0;
+    }
+    if (n) {
+        // parse the frames where they lie (zero-copy), then verify the descriptors it built
+        if (svc_quiesce(c) != 0) return -1;
+        memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
+        memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
+        VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.d_desc,
+                                     nullptr, nullptr, s.stream, nullptr, h_hsum ? s.dh_hs : nullptr),
+                  "parse launch");
+        // h_out NULL: the status bytes alone (the out words are 4 of the 5 result bytes a packet writes)
+        VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, h_out ? s.dh_out : nullptr, s.dh_status, nullptr,
+                              VPCSUM_MODE_VERIFY, nullptr, n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
+                  "verify launch");
+    }
+    VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
+    s.zero_copy = true;
+    s.svc_seq = 0;
+    s.kind = 0;
+    s.busy = true;
+    s.ticket = t;
+    s.n = n;
+    s.mode = VPCSUM_MODE_VERIFY;
+    s.user_arena = nullptr;
+    s.user_desc = nullptr;
+    s.user_out = h_out;
+    s.user_status = h_status;
+    s.user_hsum = n ? h_hsum : nullptr;
+    *ticket = t;
+    return 0;
+}
+
 int vpcsum_ctx_verify_frames(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
                              const uint32_t* h_frame_len, uint32_t n, uint32_t* h_out, uint8_t* h_status,
                              uint64_t* ticket) {
     try {
-        if (!c || !ticket) return fail("vpcsum_ctx_verify_frames: NULL context or ticket");
-        if (n > c->max_pkts) return fail("vpcsum_ctx_verify_frames: %u frames > capacity %u", n, c->max_pkts);
-        if (n && (!h_arena || !h_frame_off || !h_frame_len || !h_status))
-            return fail("vpcsum_ctx_verify_frames: NULL arena, frame table or status");
-        std::lock_guard<std::mutex> lk(c->mu);
-        VPC_ON_DEVICE(c->device);
-        uint8_t* base = n ? mapped_dev(c, h_arena, arena_len) : nullptr;
-        if (n && !base) return fail("vpcsum_ctx_verify_frames: the arena must be registered (vpcsum_ctx_register_arena)");
-        const uint64_t t = c->next_ticket++;
-        Slot& s = c->slots[t & 1];
-        if (s.busy && slot_finish(c, s) != 0) return -1;
-        if (n && c->svc.on && n <= kSvcBatchMax) {
-            // a small received batch: the service grid parses and verifies each frame
-            // (kernels.hip svc_frame_packet), the sums into its own buffer (copied out only with h_out)
-            return svc_post_frames(c, s, t, h_arena, arena_len, base, h_frame_off, h_frame_len, nullptr,
-                                   VPCSUM_F_IP | VPCSUM_F_L4, n, h_out, h_status, VPCSUM_MODE_VERIFY, false, ticket);
-        }
-        if (n) {
-            // parse the frames where they lie (zero-copy), then verify the descriptors it built
-            if (svc_quiesce(c) != 0) return -1;
-            memcpy(s.h_foff, h_frame_off, (size_t)n * 8);
-            memcpy(s.h_flen, h_frame_len, (size_t)n * 4);
-            VPC_CHECK(launch_parse_ether(base, arena_len, s.dh_foff, s.dh_flen, n, VPCSUM_F_IP | VPCSUM_F_L4, s.d_desc,
-                                         nullptr, nullptr, s.stream),
-                      "parse launch");
-            // h_out NULL: the status bytes alone (the out words are 4 of the 5 result bytes a packet writes)
-            VPC_CHECK(launch_csum(base, arena_len, s.d_desc, n, h_out ? s.dh_out : nullptr, s.dh_status, nullptr,
-                                  VPCSUM_MODE_VERIFY, nullptr, n <= kZeroCopyWaveTeams ? 12 : 0, 0, s.stream),
-                      "verify launch");
-        }
-        VPC_CHECK(hipEventRecord(s.done, s.stream), "hipEventRecord");
-        s.zero_copy = true;
-        s.svc_seq = 0;
-        s.kind = 0;
-        s.busy = true;
-        s.ticket = t;
-        s.n = n;
-        s.mode = VPCSUM_MODE_VERIFY;
-        s.user_arena = nullptr;
-        s.user_desc = nullptr;
-        s.user_out = h_out;
-        s.user_status = h_status;
-        *ticket = t;
-        return 0;
+        return ctx_verify_frames(c, h_arena, arena_len, h_frame_off, h_frame_len, n, h_out, h_status, nullptr, ticket,
+                                 "vpcsum_ctx_verify_frames");
     } VPC_CATCH("vpcsum_ctx_verify_frames")
+}
+
+int vpcsum_ctx_verify_frames_hsum(vpcsum_ctx_t* c, const uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
+                                  const uint32_t* h_frame_len, uint32_t n, uint32_t* h_out, uint8_t* h_status,
+                                  vpcsum_hsum_t* h_hsum, uint64_t* ticket) {
+    try {
+        if (n && !h_hsum) return fail("vpcsum_ctx_verify_frames_hsum: NULL header-sum array");
+        return ctx_verify_frames(c, h_arena, arena_len, h_frame_off, h_frame_len, n, h_out, h_status, h_hsum, ticket,
+                                 "vpcsum_ctx_verify_frames_hsum");
+    } VPC_CATCH("vpcsum_ctx_verify_frames_hsum")
 }
 
 int vpcsum_ctx_egress_frames(vpcsum_ctx_t* c, uint8_t* h_arena, uint64_t arena_len, const uint64_t* h_frame_off,
@@ -1510,7 +1659,9 @@ int vpcsum_ctx_pipeline(vpcsum_ctx_t* c, uint8_t* h_arena, uint32_t stride, uint
 
 struct vpcsum_group {
     std::vector<vpcsum_ctx*> ctx;
-    std::vector<uint8_t*> reg;     // arenas page-locked by the group (portable: every device maps them)
+    struct Reg { uint8_t* host; uint8_t* key; };
+    std::vector<Reg> reg;          // arenas the group registered: their page-lock references (portable
+                                   // locks: every device maps them), one per arena
     uint64_t next_ticket = 1;
     struct Pending { uint64_t ticket = 0; std::vector<uint64_t> sub; };
     Pending slots[2];
@@ -1573,9 +1724,14 @@ int vpcsum_group_destroy(vpcsum_group_t* g) {
             for (auto& slot : g->slots)
                 if (slot.ticket && vpcsum_group_wait_locked(g, slot) != 0) rc = -1;
         }
+        const int dev0 = g->ctx.empty() ? 0 : g->ctx[0]->device;   // the contexts are gone below
         for (auto* c : g->ctx)
             if (vpcsum_ctx_destroy(c) != 0) rc = -1;
-        for (auto* h : g->reg) (void)hipHostUnregister(h);
+        if (!g->reg.empty()) {
+            DeviceScope on_dev(dev0);
+            for (auto& r : g->reg)
+                if (hostlock_release(r.key, "vpcsum_group_destroy") != 0) rc = -1;
+        }
         delete g;
         return rc;
     } VPC_CATCH("vpcsum_group_destroy")
@@ -1592,7 +1748,10 @@ int vpcsum_group_register_arena(vpcsum_group_t* g, void* h_arena, uint64_t len) 
             std::lock_guard<std::mutex> lc(c->mu);
             c->registered.reserve(c->registered.size() + 1);
         }
-        VPC_CHECK(hipHostRegister(h_arena, len, hipHostRegisterMapped | hipHostRegisterPortable), "hipHostRegister");
+        for (auto& r : g->reg)
+            if (r.host == (uint8_t*)h_arena) return fail("vpcsum_group_register_arena: %p is registered already", h_arena);
+        uint8_t* key = nullptr;
+        if (hostlock_acquire((uint8_t*)h_arena, len, &key, "vpcsum_group_register_arena") != 0) return -1;
         for (size_t i = 0; i < g->ctx.size(); ++i) {
             vpcsum_ctx* c = g->ctx[i];
             std::lock_guard<std::mutex> lc(c->mu);
@@ -1607,14 +1766,14 @@ int vpcsum_group_register_arena(vpcsum_group_t* g, void* h_arena, uint64_t len) 
                     std::lock_guard<std::mutex> lq(g->ctx[q]->mu);
                     auto& rq = g->ctx[q]->registered;
                     for (size_t k = rq.size(); k-- > 0;)
-                        if (rq[k].host == (uint8_t*)h_arena && !rq[k].owned) rq.erase(rq.begin() + k);
+                        if (rq[k].host == (uint8_t*)h_arena && !rq[k].key) rq.erase(rq.begin() + k);
                 }
-                (void)hipHostUnregister(h_arena);
+                (void)hostlock_release(key, "vpcsum_group_register_arena");
                 return hipfail(e, "vpcsum_group_register_arena: device mapping");
             }
-            c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, false});
+            c->registered.push_back({(uint8_t*)h_arena, len, (uint8_t*)dev, nullptr});
         }
-        g->reg.push_back((uint8_t*)h_arena);
+        g->reg.push_back({(uint8_t*)h_arena, key});
         return 0;
     } VPC_CATCH("vpcsum_group_register_arena")
 }
@@ -1623,7 +1782,8 @@ int vpcsum_group_unregister_arena(vpcsum_group_t* g, void* h_arena) {
     try {
         if (!g || !h_arena) return fail("vpcsum_group_unregister_arena: bad argument");
         std::lock_guard<std::mutex> lk(g->mu);
-        auto it = std::find(g->reg.begin(), g->reg.end(), (uint8_t*)h_arena);
+        auto it = std::find_if(g->reg.begin(), g->reg.end(),
+                               [&](const vpcsum_group::Reg& r) { return r.host == (uint8_t*)h_arena; });
         if (it == g->reg.end()) return fail("vpcsum_group_unregister_arena: arena not registered");
         // Two phases, so that a failure leaves the registration whole and a retry can succeed:
         // (1) every context finishes its zero-copy batches -- the only step that can fail, and
@@ -1639,12 +1799,12 @@ int vpcsum_group_unregister_arena(vpcsum_group_t* g, void* h_arena) {
             std::lock_guard<std::mutex> lc(c->mu);
             auto& r = c->registered;
             for (size_t k = r.size(); k-- > 0;)
-                if (r[k].host == (uint8_t*)h_arena && !r[k].owned) r.erase(r.begin() + k);
+                if (r[k].host == (uint8_t*)h_arena && !r[k].key) r.erase(r.begin() + k);
         }
+        uint8_t* key = it->key;
         g->reg.erase(it);
         VPC_ON_DEVICE(g->ctx[0]->device);
-        VPC_CHECK(hipHostUnregister(h_arena), "hipHostUnregister");
-        return 0;
+        return hostlock_release(key, "vpcsum_group_unregister_arena");
     } VPC_CATCH("vpcsum_group_unregister_arena")
 }
 
@@ -1928,6 +2088,24 @@ int Java_io_vproxy_vpcsum_VPCsum_verifyFrames(PNIEnv_vpcsum_long* env, int64_t c
         env->return_ = (int64_t)t;
         return 0;
     } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_verifyFrames")
+}
+
+int Java_io_vproxy_vpcsum_VPCsum_verifyFramesHsum(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,
+                                                  void* frameOff, void* frameLen, int32_t n, void* out, void* status,
+                                                  void* hsum) {
+    try {
+        if (n < 0 || arenaLen < 0) {
+            fail("verifyFramesHsum: negative size");
+            return pni_throw(env, "java.lang.IllegalArgumentException");
+        }
+        uint64_t t = 0;
+        if (vpcsum_ctx_verify_frames_hsum((vpcsum_ctx_t*)(intptr_t)ctx, (const uint8_t*)arena, (uint64_t)arenaLen,
+                                          (const uint64_t*)frameOff, (const uint32_t*)frameLen, (uint32_t)n, (uint32_t*)out,
+                                          (uint8_t*)status, (vpcsum_hsum_t*)hsum, &t) != 0)
+            return pni_throw(env, "java.io.IOException");
+        env->return_ = (int64_t)t;
+        return 0;
+    } VPC_CATCH_PNI("Java_io_vproxy_vpcsum_VPCsum_verifyFramesHsum")
 }
 
 int Java_io_vproxy_vpcsum_VPCsum_egressFrames(PNIEnv_vpcsum_long* env, int64_t ctx, void* arena, int64_t arenaLen,

@@ -23,7 +23,7 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
 // no separate descriptor read over PCIe.
 constexpr int kSvcInlineDesc = 3;
 struct alignas(64) SvcMailbox {
-    uint64_t cmd;        // host: seq (bits 0..31, 0 = none yet) | n (32..55) | kSvcParse | kSvcFrames | kSvcPre | kSvcPreFmt | kSvcInline |
+    uint64_t cmd;        // host: seq (bits 0..31, 0 = none yet) | n (32..54) | kSvcHsum | kSvcParse | kSvcFrames | kSvcPre | kSvcPreFmt | kSvcInline |
                          // kSvcStop | kSvcVerify | kSvcParams
     uint64_t rsv0;
     vpcsum_desc_t idesc[kSvcInlineDesc];   // host: descriptors 0..2 of the batch, rsv = (uint8_t)seq
@@ -49,6 +49,9 @@ constexpr uint64_t kSvcFrames = 1ull << 57;
 // with kSvcFrames: parse only (vpcsum_ctx_parse_frames) -- descriptors at the aux buffer's start,
 // tuples after kSvcBatchMax descriptors, status bytes; no sums
 constexpr uint64_t kSvcParse = 1ull << 56;
+// with kSvcFrames | kSvcVerify: each frame's ingress header sum (vpcsum_hsum_t) to the aux buffer
+// (vpcsum_ctx_verify_frames_hsum)
+constexpr uint64_t kSvcHsum = 1ull << 55;
 struct SvcFrameRec {
     uint64_t off;    // the frame's offset in the arena
     uint32_t len;    // its length
@@ -57,7 +60,7 @@ struct SvcFrameRec {
     uint8_t tag;     // the inline records' batch tag (vpcsum_desc_t's rsv byte)
 };
 static_assert(sizeof(SvcFrameRec) == sizeof(vpcsum_desc_t), "a frame record takes a descriptor's slot");
-constexpr uint32_t kSvcMaxPkts = (1u << 24) - 1;   // the command's n field
+constexpr uint32_t kSvcMaxPkts = (1u << 23) - 1;   // the command's n field (bits 32..54)
 constexpr uint32_t kSvcBatchMax = 512;              // largest batch the host hands to the service (api.cpp)
 constexpr int kServiceGrid = 32;   // workgroups: 4 waves each, one packet per wave and round
 hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream);
@@ -80,7 +83,7 @@ hipError_t launch_nat_ttl_status(const uint8_t* arena, uint64_t arena_len, const
 hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const uint64_t* frame_off,
                               const uint32_t* frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* desc,
                               uint8_t* status, vpcsum_tuple_t* tuples, hipStream_t stream,
-                              const uint8_t* frame_flags = nullptr);
+                              const uint8_t* frame_flags = nullptr, vpcsum_hsum_t* hsum = nullptr);
 
 hipError_t launch_read_probe(const uint8_t* buf, uint64_t bytes, uint32_t* sink, uint32_t grid, hipStream_t stream);
 hipError_t launch_pattern_probe(const uint8_t* arena, uint64_t arena_len, const void* desc, uint32_t n, uint32_t* sink,

@@ -295,7 +295,10 @@ __device__ __forceinline__ void svc_pre_packet(const uint8_t* __restrict__ arena
     const int fld = l4_field(proto);
     const uint8_t* l3 = arena + off;
     const int r0 = (int)((uintptr_t)l3 & 15);
-    const int need = max(ver == 4 ? 20 : 40, do_l4 ? l4o + fld + 2 : l4o);
+    // the header through the L4 checksum field, or -- for a VPCSUM_PRE_HSUM entry, which is read in
+    // the same round trip -- through a TCP header of up to 60 B (options included), within the packet
+    const int len = dv.z & 0xffff;
+    const int need = max(ver == 4 ? 20 : 40, do_l4 ? max(l4o + fld + 2, min(len, l4o + 60)) : l4o);
     const int nch = (r0 + need + 15) >> 4;
     const bool win = nch <= kSvcPreChunks;
     const int npc = fmt ? 3 : 1;   // 16-B pieces of an entry
@@ -306,16 +309,23 @@ __device__ __forceinline__ void svc_pre_packet(const uint8_t* __restrict__ arena
     const uint4 e0 = shfl_u4(v, 32), e1 = shfl_u4(v, 33), e2 = shfl_u4(v, 34);
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    PreSums s = {0u, 0u, false};
+    PreSums s = {0u, 0u, false, false};
     if (tl == 0) {
         const NatRw r = fmt ? nat_rw6(e0, e1, e2) : nat_rw4(e0);
         const uint32_t sp = fmt ? e2.y : e0.w;   // the captured sum, big endian, in its top 16 bits
         const int hc = (int)(((sp >> 8) & 0xff00u) | (sp >> 24));
-        s = win ? pre_sums((const uint8_t*)&s_pw[wv][0] + r0, ver, proto, l4o, do_ip, do_l4, r, hc)
-                : pre_sums(l3, ver, proto, l4o, do_ip, do_l4, r, hc);   // a window past 384 B: byte reads
+        s = win ? pre_sums((const uint8_t*)&s_pw[wv][0] + r0, ver, proto, len, l4o, do_ip, do_l4, r, hc)
+                : pre_sums(l3, ver, proto, len, l4o, do_ip, do_l4, r, hc);   // a window past 384 B: byte reads
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");   // s_pw is the next frame's
+    if (__shfl((int)s.bad, 0, 64)) {   // a header-sum record of another packet: refused, nothing written
+        if (tl == 0) {
+            if (out) out[p] = 0;
+            if (status) status[p] = VPCSUM_S_BAD_DESC;
+        }
+        return;
+    }
     if (__shfl((int)s.udp_full, 0, 64)) {   // UDP stored 0: Java's recompute over the segment
         k1_packet<64, 4, false, true, PRED>(arena, arena_len, dv, fl & ~VPCSUM_F_PRE, true, p, out, status, arena_w, tl);
         return;
@@ -371,6 +381,14 @@ __device__ __forceinline__ void svc_frame_packet(const uint8_t* __restrict__ are
         st = parse_frame(fb, o, L, inb, (uint8_t)(rec.w & 0xffu), !VERIFY && !PARSE, d);
         dd = make_uint4((uint32_t)d.l3_off, (uint32_t)(d.l3_off >> 32), (uint32_t)d.l3_len | ((uint32_t)d.l4_off << 16),
                         (uint32_t)d.l3_ver | ((uint32_t)d.l4_proto << 8) | ((uint32_t)d.flags << 16));
+        if constexpr (VERIFY) {
+            // the ingress header sum (vpcsum_hsum_t) into the aux buffer, from the staged header
+            if (aux) {
+                const int l2 = st == 0 ? (int)(d.l3_off - o) : 0;
+                ((uint2*)aux)[p] = st == 0 ? hsum_record(fb + l2, d.l3_ver, d.l4_proto, d.l3_len, d.l4_off, l2)
+                                           : make_uint2(0u, 0u);
+            }
+        }
         if constexpr (PARSE) {
             // the descriptor, the status byte and the tuple straight to the host's buffers
             uint32_t t[10];
@@ -431,7 +449,8 @@ __device__ __forceinline__ void k1_run(const uint8_t* __restrict__ arena, uint64
             if (flags_override) fnext = flags_override[p + nteams];
         }
         if constexpr (SVC == 2) {
-            svc_frame_packet<VERIFY, PRED>(arena, arena_len, dv, p, out, status, arena_w, tl);
+            // RX verify: `pre` names the aux buffer for the frames' header sums (kSvcHsum), else NULL
+            svc_frame_packet<VERIFY, PRED>(arena, arena_len, dv, p, out, status, arena_w, tl, const_cast<void*>(pre));
         } else if constexpr (SVC == 3) {
             svc_frame_packet<false, PRED, true>(arena, arena_len, dv, p, out, status, arena_w, tl, const_cast<void*>(pre));
         } else {
@@ -1474,6 +1493,7 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         const bool rel_done = (s_par[6] & kSvcOptReleaseDone) != 0;
         const void* s_aux = (const void*)s_par[7];   // the aux buffer: pre-images, or parse results
         const void* pre = (cmd & kSvcPre) ? s_aux : nullptr;
+        const void* hsum = (cmd & kSvcHsum) ? s_aux : nullptr;   // RX verify: header sums into the aux buffer
         const int pre_fmt = (cmd & kSvcPreFmt) ? 1 : 0;
         __syncthreads();   // s_cmd / s_par are rewritten next round
         if (cmd == 0) return;
@@ -1488,7 +1508,8 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
         // round trip would serialize
         if (pred) {
             if ((cmd & kSvcVerify) && (cmd & kSvcFrames))
-                k1_run<64, 4, true, true, true, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+                k1_run<64, 4, true, true, true, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x,
+                                                   hsum);
             else if (cmd & kSvcVerify)
                 k1_run<64, 4, true, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
             else if ((cmd & kSvcFrames) && (cmd & kSvcParse))
@@ -1501,7 +1522,8 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                                                     gridDim.x, pre, pre_fmt);
         } else {
             if ((cmd & kSvcVerify) && (cmd & kSvcFrames))
-                k1_run<64, 4, true, true, false, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
+                k1_run<64, 4, true, true, false, 2>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x,
+                                                    hsum);
             else if (cmd & kSvcVerify)
                 k1_run<64, 4, true, true>(arena, alen, desc, n, out, status, nullptr, arena_w, blockIdx.x, gridDim.x);
             else if ((cmd & kSvcFrames) && (cmd & kSvcParse))
@@ -1913,7 +1935,7 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
                                                     const uint32_t* __restrict__ flen, uint32_t n, uint8_t want,
                                                     const uint8_t* __restrict__ fwant,
                                                     vpcsum_desc_t* __restrict__ desc, uint8_t* __restrict__ status,
-                                                    vpcsum_tuple_t* __restrict__ tuples) {
+                                                    vpcsum_tuple_t* __restrict__ tuples, uint2* __restrict__ hsum) {
     // 64 tuples of a wave are staged here and written as 10 coalesced 256-B stores
     __shared__ uint32_t s_tu[256 * 10];
     const uint32_t ln = threadIdx.x & 63u;
@@ -1931,6 +1953,10 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
         if (act) {
             desc[p] = d;
             if (status) status[p] = st;
+            // the ingress header sum (vpcsum_hsum_t) from the same header bytes
+            if (hsum)
+                hsum[p] = st == 0 ? hsum_record(arena + d.l3_off, d.l3_ver, d.l4_proto, d.l3_len, d.l4_off, (int)(d.l3_off - o))
+                                  : make_uint2(0u, 0u);
         }
         if (tuples) {
             // the flow tuple the L4 input nodes read (vpcsum.h vpcsum_tuple_t): addresses at
@@ -1955,12 +1981,12 @@ __global__ __launch_bounds__(256) void k_parse_ether(const uint8_t* __restrict__
 hipError_t launch_parse_ether(const uint8_t* arena, uint64_t arena_len, const uint64_t* frame_off,
                               const uint32_t* frame_len, uint32_t n, uint8_t flags, vpcsum_desc_t* desc,
                               uint8_t* status, vpcsum_tuple_t* tuples, hipStream_t stream,
-                              const uint8_t* frame_flags) {
+                              const uint8_t* frame_flags, vpcsum_hsum_t* hsum) {
     if (n == 0) return hipSuccess;
     uint32_t g = (n + 255) / 256;
     if (g > 65535u * 8) g = 65535u * 8;
     hipLaunchKernelGGL(k_parse_ether, dim3(g), dim3(256), 0, stream, arena, arena_len, frame_off, frame_len, n,
-                       flags, frame_flags, desc, status, tuples);
+                       flags, frame_flags, desc, status, tuples, (uint2*)hsum);
     return hipGetLastError();
 }
 

@@ -665,14 +665,17 @@ __global__ __launch_bounds__(256) void k_pre(uint8_t* __restrict__ arena, uint64
         for (int i = 0; i < W; ++i) {
             const uint32_t p = p0 + i * T;
             const uint64_t off = (uint64_t)dv[i].x | ((uint64_t)dv[i].y << 32);
-            const int l4o = dv[i].z >> 16;
+            const int len = dv[i].z & 0xffff, l4o = dv[i].z >> 16;
             const int ver = dv[i].w & 0xff, proto = (dv[i].w >> 8) & 0xff;
             act[i] = p < n && (((dv[i].w >> 16) & 0xff) & VPCSUM_F_PRE) != 0;
             ok[i] = act[i] && pre_desc_ok(dv[i], arena_len, FMT);
             const uintptr_t la = ok[i] ? (uintptr_t)(arena + off) : 0;
             const int r0 = (int)(la & 15);
             const bool l4 = ((dv[i].w >> 16) & VPCSUM_F_L4) != 0;
-            const int need = max(ver == 4 ? 20 : 40, l4 ? l4o + l4_field(proto) + 2 : l4o);
+            // the header through the L4 checksum field, or through the L4 header an ingress header
+            // sum covers (VPCSUM_PRE_HSUM: TCP options included)
+            const int need = max(ver == 4 ? 20 : 40,
+                                 l4 ? min(len, l4o + max(l4_field(proto) + 2, pre_hsum_hlen(rr[i]))) : l4o);
             wend[i] = ok[i] && !byte_path && r0 + need <= 16 * CH ? r0 + need : 0;
             const uint64_t base = (uint64_t)(la - (uintptr_t)r0);
             blo[i] = (uint32_t)base;
@@ -726,28 +729,31 @@ __global__ __launch_bounds__(256) void k_pre(uint8_t* __restrict__ arena, uint64
                 const int fld = l4_field(proto);
                 uint8_t* l3 = arena + off;
                 const int r0 = (int)((uintptr_t)l3 & 15);
-                PreSums s = {0u, 0u, false};
+                PreSums s = {0u, 0u, false, false};
                 if (PROBE) {
                     if (do_ip) s.ipc = ld16(w + r0 + 10);
                     if (do_l4) s.l4c = ld16(w + r0 + l4o + fld);
                 } else {
-                    s = wend[i] ? pre_sums(w + r0, ver, proto, l4o, do_ip, do_l4, rr[i])
-                                : pre_sums(l3, ver, proto, l4o, do_ip, do_l4, rr[i]);
+                    s = wend[i] ? pre_sums(w + r0, ver, proto, len, l4o, do_ip, do_l4, rr[i])
+                                : pre_sums(l3, ver, proto, len, l4o, do_ip, do_l4, rr[i]);
                     if (s.udp_full) s.l4c = udp_full_sum(l3, ver, len, l4o);
                 }
-                if (write) {
-                    // plain stores: the two fields usually share a line, which L2 writes back once
-                    // (non-temporal ones reach DRAM apart: C5 12.6 vs 18.4 Gpps)
-                    if (nt_store) {
-                        if (do_ip) st_be16_nt(l3 + 10, s.ipc);
-                        if (do_l4) st_be16_nt(l3 + l4o + fld, s.l4c);
-                    } else {
-                        if (do_ip) st_be16(l3 + 10, s.ipc);
-                        if (do_l4) st_be16(l3 + l4o + fld, s.l4c);
+                // s.bad: a header-sum record of another packet -- refused (S_BAD_DESC), nothing written
+                if (!s.bad) {
+                    if (write) {
+                        // plain stores: the two fields usually share a line, which L2 writes back once
+                        // (non-temporal ones reach DRAM apart: C5 12.6 vs 18.4 Gpps)
+                        if (nt_store) {
+                            if (do_ip) st_be16_nt(l3 + 10, s.ipc);
+                            if (do_l4) st_be16_nt(l3 + l4o + fld, s.l4c);
+                        } else {
+                            if (do_ip) st_be16(l3 + 10, s.ipc);
+                            if (do_l4) st_be16(l3 + l4o + fld, s.l4c);
+                        }
                     }
+                    res_out[i] = (s.ipc & 0xffff) | ((s.l4c & 0xffff) << 16);
+                    res_st[i] = VPCSUM_S_DONE;
                 }
-                res_out[i] = (s.ipc & 0xffff) | ((s.l4c & 0xffff) << 16);
-                res_st[i] = VPCSUM_S_DONE;
             }
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");   // the slots are rewritten for the next packet set

@@ -15,6 +15,7 @@ struct NatRw {
     uint32_t src[4], dst[4];
     uint32_t ports;   // bytes 0..1 source port, 2..3 destination port (network order)
     int mask, ttl;
+    uint32_t hs0, hs1;   // the entry's first 8 bytes: a vpcsum_hsum_t with VPCSUM_PRE_HSUM
 };
 
 __device__ __forceinline__ NatRw nat_rw4(const uint4 q) {
@@ -24,6 +25,8 @@ __device__ __forceinline__ NatRw nat_rw4(const uint4 q) {
     r.ports = q.z;
     r.mask = (int)(q.w & 0xff);
     r.ttl = (int)((q.w >> 8) & 0xff);   // rsv[0]: the VPCSUM_NAT_SET_TTL value
+    r.hs0 = q.x;
+    r.hs1 = q.y;
     return r;
 }
 __device__ __forceinline__ NatRw nat_rw6(const uint4 a, const uint4 b, const uint4 c) {
@@ -33,6 +36,8 @@ __device__ __forceinline__ NatRw nat_rw6(const uint4 a, const uint4 b, const uin
     r.ports = c.x;
     r.mask = (int)(c.y & 0xff);
     r.ttl = (int)((c.y >> 8) & 0xff);
+    r.hs0 = a.x;
+    r.hs1 = a.y;
     return r;
 }
 // big-endian 16-bit word k (bytes 2k, 2k+1) of an address / of the port pair
@@ -68,24 +73,60 @@ __device__ __forceinline__ bool pre_desc_ok(const uint4 dv, uint64_t arena_len, 
 struct PreSums {
     uint32_t ipc, l4c;
     bool udp_full;   // UDP stored 0: the caller sums the segment (udp_full_sum)
+    bool bad;        // a VPCSUM_PRE_HSUM record that does not describe this packet: nothing written
 };
 
-// One packet's sums from its L3 header at l3 (its LDS window, or the frame on the byte path) and
-// its pre-image r.
-// hc_in >= 0: the stored L4 sum as it was before this flush (the service grid's host-captured copy,
-// which keeps a re-run batch exact); otherwise it is read from the frame.
-__device__ __forceinline__ PreSums pre_sums(const uint8_t* l3, int ver, int proto, int l4o, bool do_ip, bool do_l4,
-                                            const NatRw& r, int hc_in = -1) {
-    PreSums o = {0u, 0u, false};
-    if (do_ip) {   // Ipv4Packet.__updateChecksum: the header, its own field as 0 (Ipv4Packet.java:209-217)
-        uint32_t s = 0;
-        for (int k = 0; k < l4o; k += 2)
-            if (k != 10) s += ld16(l3 + k);
-        o.ipc = 0xffff - fold32(s);
+// The ingress header sum's words (vpcsum.h vpcsum_hsum_t) of a TCP / UDP packet at l3: the
+// pseudo-header addresses (Utils.buildPseudoIPv4Header / IPv6Header, Utils.java:758-776: IPv4
+// L3+12..19, IPv6 L3+8..39) and the L4 header's 16-bit words [0, hlen) except the checksum field
+// `fld` -- every word of the L4 sum an in-place setter of the vswitch can change.  Folded end-around:
+// 0 only when every word is 0 (the per-step fold of Utils.calculateChecksumIntermediate,
+// Utils.java:783-797, gives the same value).
+__device__ __forceinline__ uint32_t hdr_words_sum(const uint8_t* l3, int ver, int l4o, int hlen, int fld) {
+    uint32_t s = 0;
+    if (ver == 4) {
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) s += ld16(l3 + 12 + k);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 32; k += 2) s += ld16(l3 + 8 + k);
     }
-    if (!do_l4) return o;
-    // the L4 sum's words a rewrite changes: the pseudo-header addresses of TCP / UDP and ICMPv6 (an
-    // ICMPv4 message has no pseudo header, inside IPv6 too) and the TCP / UDP ports (nat_setters)
+    for (int k = 0; k < hlen; k += 2)
+        if (k != fld) s += ld16(l3 + l4o + k);
+    return fold32(s);
+}
+
+// A parsed packet's vpcsum_hsum_t as two dwords (bytes 0..3, 4..7), from its L3 bytes at l3:
+// {sum, l4_len} and {hlen, proto, ver, l2_len}; zeros (no record) unless it is TCP with a data
+// offset of 20..seg bytes or UDP with its 8-B header in the segment.
+__device__ __forceinline__ uint2 hsum_record(const uint8_t* l3, int ver, int proto, int len, int l4o, int l2) {
+    const int seg = len - l4o;
+    int hlen;
+    if (proto == 6) {
+        if (seg < 20) return make_uint2(0u, 0u);
+        hlen = (l3[l4o + 12] >> 4) * 4;
+        if (hlen < 20 || hlen > seg) return make_uint2(0u, 0u);
+    } else if (proto == 17) {
+        if (seg < 8) return make_uint2(0u, 0u);
+        hlen = 8;
+    } else {
+        return make_uint2(0u, 0u);
+    }
+    const uint32_t s = hdr_words_sum(l3, ver, l4o, hlen, l4_field(proto));
+    return make_uint2(s | ((uint32_t)seg << 16),
+                      (uint32_t)hlen | ((uint32_t)proto << 8) | ((uint32_t)ver << 16) | ((uint32_t)l2 << 24));
+}
+
+// The L4 header length a VPCSUM_PRE_HSUM entry asks for (0: not such an entry); the window a
+// pre-image kernel loads must reach l4o + this.
+__device__ __forceinline__ int pre_hsum_hlen(const NatRw& r) {
+    return (r.mask & VPCSUM_PRE_HSUM) ? (int)(r.hs1 & 0xff) : 0;
+}
+
+// RFC 1624's sum(~m + m') over the words a NAT entry records: the pseudo-header addresses of TCP /
+// UDP and ICMPv6 (an ICMPv4 message has no pseudo header, inside IPv6 too) and the TCP / UDP ports
+// (nat_setters); m from the entry, m' from the frame.
+__device__ __forceinline__ uint32_t nat_words_diff(const uint8_t* l3, int ver, int proto, int l4o, const NatRw& r) {
     const bool ports = proto == 6 || proto == 17;
     const bool addr = ports || (ver == 6 && proto == 58);
     uint32_t diff = 0;
@@ -106,6 +147,40 @@ __device__ __forceinline__ PreSums pre_sums(const uint8_t* l3, int ver, int prot
     if (ports) {
         if (r.mask & VPCSUM_NAT_SPORT) diff += (~rw_word(&r.ports, 0) & 0xffff) + ld16(l3 + l4o);
         if (r.mask & VPCSUM_NAT_DPORT) diff += (~rw_word(&r.ports, 1) & 0xffff) + ld16(l3 + l4o + 2);
+    }
+    return diff;
+}
+
+// One packet's sums from its L3 header at l3 (its LDS window, or the frame on the byte path) and
+// its pre-image r.
+// hc_in >= 0: the stored L4 sum as it was before this flush (the service grid's host-captured copy,
+// which keeps a re-run batch exact); otherwise it is read from the frame.
+__device__ __forceinline__ PreSums pre_sums(const uint8_t* l3, int ver, int proto, int len, int l4o, bool do_ip,
+                                            bool do_l4, const NatRw& r, int hc_in = -1) {
+    PreSums o = {0u, 0u, false, false};
+    if (do_ip) {   // Ipv4Packet.__updateChecksum: the header, its own field as 0 (Ipv4Packet.java:209-217)
+        uint32_t s = 0;
+        for (int k = 0; k < l4o; k += 2)
+            if (k != 10) s += ld16(l3 + k);
+        o.ipc = 0xffff - fold32(s);
+    }
+    if (!do_l4) return o;
+    uint32_t diff = 0;
+    if (r.mask & VPCSUM_PRE_HSUM) {
+        // the header as one word: ~m = the recorded header sum's complement, m' = the same words
+        // now.  Only for the packet the record describes: same version and protocol, same segment
+        // length (the pseudo header's length word and the payload's place), same header length
+        // (a TCP option list rebuilt in place would move the payload)
+        const int hlen = (int)(r.hs1 & 0xff);
+        const int cur = proto == 6 ? (l3[l4o + 12] >> 4) * 4 : 8;
+        if ((r.hs1 >> 24) == 0 || (int)((r.hs1 >> 16) & 0xff) != ver || (int)((r.hs1 >> 8) & 0xff) != proto ||
+            (int)(r.hs0 >> 16) != len - l4o || hlen != cur || hlen > len - l4o || !(proto == 6 || proto == 17)) {
+            o.bad = true;
+            return o;
+        }
+        diff = (~r.hs0 & 0xffff) + hdr_words_sum(l3, ver, l4o, hlen, l4_field(proto));
+    } else {
+        diff = nat_words_diff(l3, ver, proto, l4o, r);
     }
     const uint32_t hc = hc_in >= 0 ? (uint32_t)hc_in : ld16(l3 + l4o + l4_field(proto));
     if (proto == 17 && hc == 0) {   // "no checksum": Java's recompute writes a real one (UdpPacket.java:136-164)

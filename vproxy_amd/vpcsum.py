@@ -23,7 +23,8 @@ MODE_COMPUTE, MODE_VERIFY, MODE_WRITE = 0x00, 0x01, 0x10
 NAT_SRC, NAT_DST, NAT_SPORT, NAT_DPORT, NAT_DEC_TTL, NAT_SET_TTL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 NAT_RFC1624, NAT_STRICT_JAVA = 0x00, 0x01
 PRE_FMT_PRE4, PRE_FMT_PRE = 0, 1   # pre-image entries: NAT4_DTYPE (16 B, IPv4) / NAT_DTYPE (48 B)
-ABI_VERSION = 3   # include/vpcsum.h VPCSUM_ABI_VERSION: the library this binding was written against
+PRE_HSUM = 0x80   # pre-image entry mask: the entry's first 8 bytes hold an HSUM_DTYPE record
+ABI_VERSION = 4   # include/vpcsum.h VPCSUM_ABI_VERSION: the library this binding was written against
 SYNTH_C1, SYNTH_C2, SYNTH_C3, SYNTH_C4, SYNTH_FUZZ, SYNTH_C5 = 1, 2, 3, 4, 5, 6
 
 DESC_DTYPE = np.dtype([("l3_off", "<u8"), ("l3_len", "<u2"), ("l4_off", "<u2"), ("l3_ver", "u1"),
@@ -36,6 +37,9 @@ NAT4R_DTYPE = np.dtype([("desc", DESC_DTYPE), ("rw", NAT4_DTYPE)])   # vpcsum_na
 # vpcsum_tuple_t: the flow tuple of a parsed frame (network-order addresses and ports)
 TUPLE_DTYPE = np.dtype([("src", "u1", 16), ("dst", "u1", 16), ("sport", "u1", 2), ("dport", "u1", 2),
                         ("l3_ver", "u1"), ("l4_proto", "u1"), ("tcp_flags", "u1"), ("rsv", "u1")])
+# vpcsum_hsum_t: a received TCP / UDP frame's ingress header sum (l2_len 0: no record)
+HSUM_DTYPE = np.dtype([("sum", "<u2"), ("l4_len", "<u2"), ("hlen", "u1"), ("l4_proto", "u1"), ("l3_ver", "u1"),
+                       ("l2_len", "u1")])
 
 # Every symbol include/vpcsum.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -59,6 +63,7 @@ EXPORTS = [
     "Java_io_vproxy_vpcsum_VPCsum_submit", "Java_io_vproxy_vpcsum_VPCsum_waitFor",
     "Java_io_vproxy_vpcsum_VPCsum_close", "Java_io_vproxy_vpcsum_VPCsum_setService",
     "Java_io_vproxy_vpcsum_VPCsum_verifyFrames", "Java_io_vproxy_vpcsum_VPCsum_parseFrames",
+    "vpcsum_ctx_verify_frames_hsum", "vpcsum_parse_ether_hsum_async", "Java_io_vproxy_vpcsum_VPCsum_verifyFramesHsum",
 ]
 
 
@@ -72,6 +77,82 @@ class VpcsumError(RuntimeError):
 
 _lib = None
 _lock = threading.Lock()
+
+# Host ranges this binding page-locked (ptr -> nbytes, counted per registration) and the ranges it
+# released since the last `released_ranges(clear=True)`: the GPU tests' audit checks that HIP no
+# longer holds a released range as registered (tests/conftest.py, tests/hiputil.py).
+_live_regs: dict[int, list[int]] = {}
+_released: list[tuple[int, int]] = []
+_leaked: list[dict] = []   # arrays of a context / group whose destroy failed: kept alive
+
+
+# VPCSUM_AUDIT_REGISTRATIONS=1 (the GPU tests set it): right after each release, while the array
+# is still referenced, ask HIP whether it still holds the range as page-locked; any that it does is
+# recorded in _stale (a registration outliving its release: a later pageable copy from memory
+# allocated at those addresses would go through its dead mapping).
+_AUDIT = os.environ.get("VPCSUM_AUDIT_REGISTRATIONS") == "1"
+_stale: list[tuple[int, int]] = []
+_hip = None
+
+
+class _PtrAttr(ctypes.Structure):   # hipPointerAttribute_t (hip_runtime_api.h)
+    _fields_ = [("type", ctypes.c_int), ("device", ctypes.c_int), ("devicePointer", ctypes.c_void_p),
+                ("hostPointer", ctypes.c_void_p), ("isManaged", ctypes.c_int), ("allocationFlags", ctypes.c_uint)]
+
+
+def hip_holds_registered(ptr: int) -> bool:
+    """Whether the HIP runtime (the libamdhip64 this process loaded) holds host address `ptr` as
+    page-locked memory (hipPointerGetAttributes: hipMemoryTypeHost)."""
+    global _hip
+    if _hip is None:
+        lib()
+        path = None
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64.so" in line:
+                    path = line.split()[-1]
+                    break
+        if path is None:
+            raise VpcsumUnavailable("libamdhip64 is not loaded")
+        h = ctypes.CDLL(path)
+        h.hipPointerGetAttributes.argtypes = [ctypes.POINTER(_PtrAttr), ctypes.c_void_p]
+        h.hipPointerGetAttributes.restype = ctypes.c_int
+        h.hipGetLastError.restype = ctypes.c_int
+        _hip = h
+    a = _PtrAttr()
+    rc = _hip.hipPointerGetAttributes(ctypes.byref(a), ctypes.c_void_p(ptr))
+    _hip.hipGetLastError()   # an unknown pointer leaves hipErrorInvalidValue behind
+    return rc == 0 and a.type == 1
+
+
+def _reg_add(ptr: int, nbytes: int):
+    with _lock:
+        _live_regs.setdefault(ptr, []).append(nbytes)
+
+
+def _reg_drop(ptr: int):
+    with _lock:
+        lst = _live_regs.get(ptr)
+        if not lst:
+            return
+        n = lst.pop()
+        _released.append((ptr, n))
+        if not lst:
+            del _live_regs[ptr]
+        covered = any(q <= ptr < q + max(m) for q, m in _live_regs.items())
+    if _AUDIT and not covered and (hip_holds_registered(ptr) or hip_holds_registered(ptr + n - 1)):
+        _stale.append((ptr, n))
+
+
+def released_ranges(clear: bool = True) -> list[tuple[int, int]]:
+    """Ranges released (unregistered, or their context / group destroyed) that no registration of
+    this binding covers any more."""
+    with _lock:
+        out = [(p, n) for p, n in _released
+               if not any(q <= p < q + max(m) for q, m in _live_regs.items())]
+        if clear:
+            _released.clear()
+        return out
 
 
 def _declare(L):
@@ -107,6 +188,7 @@ def _declare(L):
         "vpcsum_batch_wait": ([U64], I),
         "vpcsum_parse_ether_async": ([P, U64, P, P, U32, U8, P, P, P], I),
         "vpcsum_parse_ether_tuples_async": ([P, U64, P, P, U32, U8, P, P, P, P], I),
+        "vpcsum_parse_ether_hsum_async": ([P, U64, P, P, U32, U8, P, P, P, P], I),
         "vpcsum_read_probe_async": ([P, U64, P, U32, P], I),
         "vpcsum_pattern_probe_async": ([P, U64, P, U32, P, U32, P], I),
         "vpcsum_nat4_pattern_probe_async": ([P, U64, P, P, U32, P], I),
@@ -123,6 +205,7 @@ def _declare(L):
         "vpcsum_ctx_set_service": ([P, U32], I),
         "vpcsum_ctx_stats": ([P, P, P], I),
         "vpcsum_ctx_verify_frames": ([P, P, U64, P, P, U32, P, P, P], I),
+        "vpcsum_ctx_verify_frames_hsum": ([P, P, U64, P, P, U32, P, P, P, P], I),
         "vpcsum_ctx_parse_frames": ([P, P, U64, P, P, U32, P, P, P, P], I),
         "vpcsum_ctx_egress_frames": ([P, P, U64, P, P, P, U32, P, P, P], I),
         "vpcsum_ctx_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
@@ -217,9 +300,16 @@ def pre(arena, desc, pre_img, n: int, out=None, status=None, mode: int = MODE_WR
 
 
 def parse_ether(arena, frame_off, frame_len, n: int, desc, status=None, flags: int = F_IP | F_L4, stream=None,
-                tuples=None):
+                tuples=None, hsum=None):
     """Descriptors from raw frames on the GPU; with `tuples` (n x 40 bytes, TUPLE_DTYPE) also each
-    frame's flow tuple (vpcsum_parse_ether_tuples_async)."""
+    frame's flow tuple (vpcsum_parse_ether_tuples_async); with `hsum` (n x 8 bytes, HSUM_DTYPE) each
+    frame's ingress header sum instead (vpcsum_parse_ether_hsum_async)."""
+    if hsum is not None:
+        assert tuples is None and hsum.numel() * hsum.element_size() >= n * HSUM_DTYPE.itemsize
+        _check(lib().vpcsum_parse_ether_hsum_async(_ptr(arena), arena.numel(), _ptr(frame_off), _ptr(frame_len), n,
+                                                   flags, _ptr(desc), _ptr(status), _ptr(hsum), _stream(stream)),
+               "vpcsum_parse_ether_hsum_async")
+        return
     if tuples is None:
         _check(lib().vpcsum_parse_ether_async(_ptr(arena), arena.numel(), _ptr(frame_off), _ptr(frame_len), n, flags,
                                               _ptr(desc), _ptr(status), _stream(stream)), "vpcsum_parse_ether_async")
@@ -307,10 +397,12 @@ class Context:
     def register(self, arr: np.ndarray):
         _check(lib().vpcsum_ctx_register_arena(self.h, arr.ctypes.data, arr.nbytes), "vpcsum_ctx_register_arena")
         self._pinned[arr.ctypes.data] = arr
+        _reg_add(arr.ctypes.data, arr.nbytes)
 
     def unregister(self, arr: np.ndarray):
         _check(lib().vpcsum_ctx_unregister_arena(self.h, arr.ctypes.data), "vpcsum_ctx_unregister_arena")
         self._pinned.pop(arr.ctypes.data, None)
+        _reg_drop(arr.ctypes.data)
 
     def submit(self, arena: np.ndarray, desc: np.ndarray, out: np.ndarray | None, status: np.ndarray | None = None,
                mode: int = MODE_COMPUTE) -> int:
@@ -362,6 +454,22 @@ class Context:
                "vpcsum_ctx_verify_frames")
         self.wait(t.value)
         return out, status
+
+    def verify_frames_hsum(self, arena: np.ndarray, frame_off: np.ndarray, frame_len: np.ndarray):
+        """verify_frames(sums=False) that also records each frame's ingress header sum
+        (vpcsum_ctx_verify_frames_hsum, GpuCsumBatch.verifyFrames' form since ABI 4).  Returns
+        (status, hsum): S_* bytes and HSUM_DTYPE records per frame."""
+        n = len(frame_off)
+        fo = np.ascontiguousarray(frame_off, dtype=np.uint64)
+        fl = np.ascontiguousarray(frame_len, dtype=np.uint32)
+        status = np.zeros(n, np.uint8)
+        hsum = np.zeros(n, HSUM_DTYPE)
+        t = ctypes.c_uint64()
+        _check(lib().vpcsum_ctx_verify_frames_hsum(self.h, arena.ctypes.data, arena.nbytes, fo.ctypes.data,
+                                                   fl.ctypes.data, n, None, status.ctypes.data, hsum.ctypes.data,
+                                                   ctypes.byref(t)), "vpcsum_ctx_verify_frames_hsum")
+        self.wait(t.value)
+        return status, hsum
 
     def parse_frames(self, arena: np.ndarray, frame_off: np.ndarray, frame_len: np.ndarray):
         """Batched parse of received Ethernet frames in a registered arena, with flow tuples
@@ -434,9 +542,17 @@ class Context:
                                          out.ctypes.data, mode, chunks), "vpcsum_ctx_pipeline")
 
     def close(self):
+        """Destroy the context (its batches finish, its page-locks go).  If an unregister failed,
+        the arrays it held stay referenced (never freed while HIP may still map them) and the error
+        is raised."""
         if self.h:
-            lib().vpcsum_ctx_destroy(self.h)
+            rc = lib().vpcsum_ctx_destroy(self.h)
             self.h = None
+            if rc != 0:
+                _leaked.append(self._pinned.copy())
+                _check(rc, "vpcsum_ctx_destroy")
+            for p in self._pinned:
+                _reg_drop(p)
             self._pinned.clear()
             self._inflight.clear()
 
@@ -463,10 +579,12 @@ class Group:
     def register(self, arr: np.ndarray):
         _check(lib().vpcsum_group_register_arena(self.h, arr.ctypes.data, arr.nbytes), "vpcsum_group_register_arena")
         self._pinned[arr.ctypes.data] = arr
+        _reg_add(arr.ctypes.data, arr.nbytes)
 
     def unregister(self, arr: np.ndarray):
         _check(lib().vpcsum_group_unregister_arena(self.h, arr.ctypes.data), "vpcsum_group_unregister_arena")
         self._pinned.pop(arr.ctypes.data, None)
+        _reg_drop(arr.ctypes.data)
 
     def submit(self, arena: np.ndarray, desc: np.ndarray, out: np.ndarray, status: np.ndarray | None = None,
                mode: int = MODE_COMPUTE) -> int:
@@ -512,8 +630,13 @@ class Group:
 
     def close(self):
         if self.h:
-            lib().vpcsum_group_destroy(self.h)
+            rc = lib().vpcsum_group_destroy(self.h)
             self.h = None
+            if rc != 0:
+                _leaked.append(self._pinned.copy())
+                _check(rc, "vpcsum_group_destroy")
+            for p in self._pinned:
+                _reg_drop(p)
             self._pinned.clear()
             self._inflight.clear()
 

@@ -133,11 +133,151 @@ def record_pre_image(arena, l3_off: int, ver: int, l4_off: int, proto: int, mask
     return e
 
 
+def hsum_entry(rec) -> np.void:
+    """The 48-B pre-image entry (NAT_DTYPE, mask PRE_HSUM) that carries a frame's ingress header
+    sum (HSUM_DTYPE record, from Context.verify_frames_hsum) to the egress flush: the record in
+    its first 8 bytes (GpuCsumBatch.defer, java/io/vproxy/vpcsum/PreImage.java:writeTo)."""
+    raw = np.zeros(48, np.uint8)
+    raw[:8] = np.frombuffer(np.asarray(rec, V.HSUM_DTYPE).tobytes(), np.uint8)
+    raw[36] = V.PRE_HSUM
+    return raw.view(V.NAT_DTYPE)[0]
+
+
+def hsum_eligible(rx_status: int, rec, l3_rx: int, in_place: bool, l3_now: int, ver: int, proto: int, l3_len: int,
+                  l4_off: int, tcp_hlen: int) -> bool:
+    """GpuCsumBatch.defer's rule for F_PRE: a frame whose L4 sum is dirty
+    takes the header-sum update instead of the full recompute only when
+      * the ingress verify proved its stored L4 sum (S_L4_OK, no S_BAD_DESC) and recorded its header
+        sum (l2_len != 0);
+      * it leaves from the zero-copy branch of XDPIface.sendPacket with its bytes still the received
+        frame (`in_place`: pkb.fullbuf is still the RX chunk -- any clearRawPacket on the packet or
+        its layers, e.g. TcpPacket.setData / setOptions / the MSS option added by
+        SwitchUtils.checkAndUpdateMss, and PacketBuffer.replacePacket null it, AbstractPacket.java:
+        27-36, PacketBuffer.java:199-253) and its L3 header where it was received (`l3_now` ==
+        `l3_rx`: a decapsulated inner frame or a moved header never matches);
+      * its version, protocol, segment length and L4 header length (the TCP data offset the packet
+        object now reports) are the record's.
+    Then every byte outside the header words the record sums is the received byte, so the update is
+    exact whatever the in-place setters wrote into those words (addresses, ports, sequence and
+    acknowledgement numbers, flags, an option's data)."""
+    if (rx_status & (V.S_L4_OK | V.S_BAD_DESC)) != V.S_L4_OK or int(rec["l2_len"]) == 0:
+        return False
+    if not in_place or l3_now != l3_rx:
+        return False
+    if int(rec["l3_ver"]) != ver or int(rec["l4_proto"]) != proto or int(rec["l4_len"]) != l3_len - l4_off:
+        return False
+    return proto == 17 and int(rec["hlen"]) == 8 or proto == 6 and int(rec["hlen"]) == tcp_hlen
+
+
 def pre_eligible(rx_status: int) -> bool:
     """Whether a NAT'd frame's L4 sum may be updated from its pre-image at egress: ingress verify
     proved the stored L4 sum correct (S_L4_OK; a UDP stored 0 never carries it).  Otherwise the
     frame takes the full recompute, as Java's getRawPacket(0) does (AbstractPacket.java:58-65)."""
     return (rx_status & V.S_BAD_DESC) == 0 and (rx_status & V.S_L4_OK) != 0
+
+
+class RxPacket:
+    """A received frame as the vswitch holds it between XDPIface.readable and sendPacket: its
+    PacketBuffer with the fields the integration adds (csumStatus, csumHsum, csumL3: the verify
+    status, the ingress header sum and the L3 header's umem offset) and the byte
+    effects of the packet objects' setters on the umem frame.
+
+    The in-place setters (the `raw != null` branch of TcpPacket.setSrcPort / setDstPort /
+    setSeqNum / setAckNum / setFlags, TcpPacket.java:31-100; TcpOption.setData of a same-length
+    option, :561-569; UdpPacket.setSrcPort / setDstPort, UdpPacket.java:188-209; Ipv4Packet.setSrc /
+    setDst / setTtl, Ipv4Packet.java:401-458; Ipv6Packet.setSrc / setDst) write the frame's bytes
+    and mark sums dirty.  Every other change rebuilds the packet (clearRawPacket, which clears the
+    PacketBuffer's buffers up the parent chain, AbstractPacket.java:27-36, PacketBuffer.java:
+    199-208): the frame then leaves through XDPIface.sendPacket's copying branch from another chunk
+    (:139-168) -- :meth:`rebuild` -- and PacketBuffer.replacePacket (TcpReset, TcpStack, the ICMP
+    answers) also resets the integration's fields -- :meth:`replace`."""
+
+    def __init__(self, arena: np.ndarray, frame_off: int, rx_status: int, hsum_rec):
+        self.arena = arena
+        self.frame_off = frame_off
+        self.csum_status = int(rx_status)
+        self.csum_hsum = np.asarray(hsum_rec, V.HSUM_DTYPE).copy()
+        l2 = int(self.csum_hsum["l2_len"])
+        self.csum_l3 = frame_off + l2 if l2 else -1
+        self.in_place = True      # pkb.fullbuf is still the RX chunk (the zero-copy send branch)
+        self.ip_dirty = self.l4_dirty = False
+        d = egress_descriptor(arena[frame_off:frame_off + 512], frame_off, 0)
+        self.l3 = int(d["l3_off"])
+        self.ver, self.proto = int(d["l3_ver"]), int(d["l4_proto"])
+        self.l4 = self.l3 + int(d["l4_off"])
+
+    # -- in-place setters ------------------------------------------------------------------
+    def _pseudo_dirty(self):
+        self.ip_dirty = self.ip_dirty or self.ver == 4
+        self.l4_dirty = self.l4_dirty or self.proto in (6, 17)
+
+    def set_src(self, addr: bytes):
+        a, n = (self.l3 + 12, 4) if self.ver == 4 else (self.l3 + 8, 16)
+        self.arena[a:a + n] = np.frombuffer(addr[:n], np.uint8)
+        self._pseudo_dirty()
+
+    def set_dst(self, addr: bytes):
+        a, n = (self.l3 + 16, 4) if self.ver == 4 else (self.l3 + 24, 16)
+        self.arena[a:a + n] = np.frombuffer(addr[:n], np.uint8)
+        self._pseudo_dirty()
+
+    def _l4_write(self, off: int, data: bytes):
+        self.arena[self.l4 + off:self.l4 + off + len(data)] = np.frombuffer(data, np.uint8)
+        self.l4_dirty = True
+
+    def set_ports(self, sport: int, dport: int):
+        self._l4_write(0, sport.to_bytes(2, "big") + dport.to_bytes(2, "big"))
+
+    def set_seq(self, v: int):
+        self._l4_write(4, (v & 0xFFFFFFFF).to_bytes(4, "big"))
+
+    def set_ack(self, v: int):
+        self._l4_write(8, (v & 0xFFFFFFFF).to_bytes(4, "big"))
+
+    def set_tcp_flags(self, flags: int):
+        """TcpPacket.setFlags in place (TcpPacket.java:90-96): the low 6 bits of the word at 12."""
+        w = (int(self.arena[self.l4 + 12]) << 8 | int(self.arena[self.l4 + 13])) & 0xFFC0 | (flags & 0x3F)
+        self._l4_write(12, w.to_bytes(2, "big"))
+
+    def set_option_data(self, opt_off: int, data: bytes):
+        """TcpOption.setData of an option of the same length: its data bytes at option + 2."""
+        self._l4_write(opt_off + 2, data)
+
+    def set_ttl(self, ttl: int):
+        if self.ver == 4:
+            self.arena[self.l3 + 8] = ttl
+            self.ip_dirty = True
+        else:
+            self.arena[self.l3 + 7] = ttl   # Ipv6Packet.setHopLimit: no sum covers it
+
+    # -- rebuilds --------------------------------------------------------------------------
+    def rebuild(self, new_off: int, frame: bytes):
+        """The packet was rebuilt (clearRawPacket): sendPacket copies its new bytes to another
+        chunk; every sum of the new bytes is Java's to compute."""
+        self.arena[new_off:new_off + len(frame)] = np.frombuffer(frame, np.uint8)
+        self.__init_moved(new_off)
+
+    def replace(self, new_off: int, frame: bytes):
+        """PacketBuffer.replacePacket / clearAndSetPacket: a new packet in the same PacketBuffer
+        (TcpReset.java:82 and the other callers); clearPackets resets csumStatus / csumHsum / csumL3."""
+        self.csum_status, self.csum_l3 = -1, -1
+        self.csum_hsum = np.zeros((), V.HSUM_DTYPE)
+        self.rebuild(new_off, frame)
+
+    def __init_moved(self, new_off: int):
+        self.frame_off = new_off
+        self.in_place = False
+        d = egress_descriptor(self.arena[new_off:new_off + 512], new_off, 0)
+        self.l3 = int(d["l3_off"])
+        self.ver, self.proto = int(d["l3_ver"]), int(d["l4_proto"])
+        self.l4 = self.l3 + int(d["l4_off"])
+        self.ip_dirty = self.ver == 4
+        self.l4_dirty = self.proto in L4_WITH_CSUM
+
+    def tcp_hlen(self) -> int:
+        """The TCP header length now in the frame (data offset nibble of byte 12 * 4; GpuCsumBatch
+        reads the umem byte: a partially parsed TcpPacket has no getDataOffset(), :186-199)."""
+        return (int(self.arena[self.l4 + 12]) >> 4) * 4 if self.proto == 6 else 0
 
 
 class EgressBatch:
@@ -204,6 +344,32 @@ class EgressBatch:
             else:
                 self.stats["pre_full"] += 1
         self.desc[self.n] = (l3_off, l3_len, l4_off, ver, proto, flags, 0)
+        self.n += 1
+        self.stats["deferred"] += 1
+        return True
+
+    def defer_rx(self, pkt: RxPacket) -> bool:
+        """GpuCsumBatch.defer for a received packet the vswitch is sending (XDPIface.sendPacket):
+        its dirty sums from the setters that ran, the descriptor from the IP header fields, and
+        F_PRE with the frame's ingress header sum when :func:`hsum_eligible` holds -- otherwise a
+        frame that carries a record is summed in full (`pre_full`)."""
+        flags = checksum_flags_for(pkt.ver == 4, pkt.ip_dirty, pkt.proto, pkt.l4_dirty)
+        if not self._take(flags):
+            return False
+        d = egress_descriptor(self.arena[pkt.frame_off:pkt.frame_off + 512], pkt.frame_off, flags)
+        if d is None:
+            return False
+        if self.n == self.capacity:
+            self.complete_tx()
+        if flags & V.F_L4 and int(pkt.csum_hsum["l2_len"]):
+            if hsum_eligible(pkt.csum_status, pkt.csum_hsum, pkt.csum_l3, pkt.in_place, int(d["l3_off"]),
+                             int(d["l3_ver"]), int(d["l4_proto"]), int(d["l3_len"]), int(d["l4_off"]), pkt.tcp_hlen()):
+                d["flags"] |= V.F_PRE
+                self.pre[self.n] = hsum_entry(pkt.csum_hsum)
+                self.stats["pre_deferred"] += 1
+            else:
+                self.stats["pre_full"] += 1
+        self.desc[self.n] = d
         self.n += 1
         self.stats["deferred"] += 1
         return True
