@@ -35,8 +35,10 @@ def V():
 
 
 def dev(a):
+    """A pageable host-to-device copy (torch's plain `.cuda()`), the path round 5's two intermittent
+    faults hit; round 6 restores it here (DESIGN_HISTORY.md "Round 6: the intermittent fault")."""
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).pin_memory().cuda()
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()
 
 
 def pre_images(arena, desc, rw):
