@@ -406,11 +406,12 @@ def main():
         evs[i + 1].record(stream)
     torch.cuda.synchronize()
     per_launch = [evs[i].elapsed_ms(evs[i + 1]) for i in range(args.steps)]
-    # The same K steps with two batches in flight: the launches alternate between the kernel's
-    # stream and a second one (each with its own out words), so that one launch's ramp and drain
-    # overlap its neighbour's -- the rate of a caller that keeps two batches in flight, as the
-    # device group and the host contexts do.  Reported next to `value`, not as it: the roofline
-    # prices a launch alone, and overlapped launches have no duration of their own.
+    # The same K steps with two batches in flight, through the library's pipe (vpcsum_pipe_*: the
+    # launches alternate between the pipe's two streams, forked from the kernel's stream and joined
+    # back into it; each batch with its own out words), so that one launch's ramp and drain overlap
+    # its neighbour's -- the rate of a caller that keeps two batches in flight, as the host contexts
+    # do with their two slots.  Reported next to `value`, not as it: the roofline prices a launch
+    # alone, and overlapped launches have no duration of their own.
     peak_main = int(torch.cuda.max_memory_allocated())   # before the second batch below
     pipe_wall, pipe_bytes = 0.0, 0.0
     if not nat:
@@ -422,26 +423,32 @@ def main():
                 d2 = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
                 V.synth(a2, n, stride, 0, synth_id, SEED, first + world * n_cfg, d2, stream=stream)
                 pb = [(arena, d, bytes_per_step), (a2, d2, algorithmic_bytes(V.tensor_to_desc(d2)[:n]))]
-            s2 = torch.cuda.Stream()
+            pipe = V.Pipe(stream)
             out2 = torch.zeros_like(out)
 
             def step2(i):
                 a, dd, _ = pb[i % len(pb)]
-                V.compute(a, dd, n, (out, out2)[i % 2], None, V.MODE_COMPUTE, args.team, stream=(stream, s2)[i % 2])
+                pipe.compute(a, dd, n, (out, out2)[i % 2], None, V.MODE_COMPUTE, args.team)
+            pipe.begin()
             for i in range(4):
                 step2(i)
+            pipe.join()
             pipe_bytes = float(sum(pb[i % len(pb)][2] for i in range(args.steps)))
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         if n:
+            pipe.begin()
             for i in range(args.steps):
                 step2(i)
+            pipe.join()
         torch.cuda.synchronize()
         pipe_wall = max_over_ranks(time.perf_counter() - t0)
         pipe_bytes = sum_over_ranks(pipe_bytes)
         pb = a2 = d2 = None
+        if n:
+            pipe.close()
     wall_max = max_over_ranks(wall)
     # per-rank attribution of a multi-GPU line: every rank's kernel time and the card it ran on
     props = torch.cuda.get_device_properties(torch.cuda.current_device())
@@ -679,8 +686,9 @@ def main():
             line["pipelined_two_streams"] = {"value": round(pv, 2), "unit": "GB/s",
                                              "ms_per_step": round(pipe_wall / args.steps * 1e3, 5),
                                              "over_value": round(pv / value, 4),
-                                             "what": "the same K steps alternating two streams (two batches in "
-                                                     "flight); not `value`: the roofline prices one launch alone"}
+                                             "api": "vpcsum_pipe_begin / vpcsum_pipe_compute_async / vpcsum_pipe_join",
+                                             "what": "the same K steps with two batches in flight through the "
+                                                     "library's pipe; not `value`: the roofline prices one launch alone"}
         if nat:
             line["config"]["Mpps_rank0"] = round(n / kernel_ms / 1e3, 1) if n else 0
         print(json.dumps(line), flush=True)

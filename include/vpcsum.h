@@ -213,6 +213,24 @@ int vpcsum_compute_async(const uint8_t* d_arena, uint64_t arena_len,
                          uint32_t* d_out, uint8_t* d_status,
                          uint32_t mode, void* stream);
 
+/* Two batches in flight.  A launch spends its first and last microseconds
+ * ramping up and draining; a caller that keeps two batches in flight overlaps those with its
+ * neighbour's steady state (C1, 64-B frames: +29%).  A pipe owns two streams on the
+ * caller's device: vpcsum_pipe_begin forks them from `stream` (they wait for the work queued on it
+ * so far), each vpcsum_pipe_compute_async (vpcsum_compute_async's arguments) goes to the next of the
+ * two in turn, so consecutive batches may run concurrently -- their out / status / written frames
+ * must not overlap -- and vpcsum_pipe_join makes `stream` wait for every batch launched since.  The
+ * host contexts do the same on their own: each keeps two slots, each with its stream, and a submit
+ * goes to the other slot than the last (wait for ticket t before reusing t's buffers). */
+typedef struct vpcsum_pipe vpcsum_pipe_t;
+int vpcsum_pipe_create(void* stream, vpcsum_pipe_t** out);
+int vpcsum_pipe_begin(vpcsum_pipe_t* pipe);
+int vpcsum_pipe_compute_async(vpcsum_pipe_t* pipe, const uint8_t* d_arena, uint64_t arena_len,
+                              const vpcsum_desc_t* d_desc, uint32_t n, uint32_t* d_out, uint8_t* d_status,
+                              uint32_t mode);
+int vpcsum_pipe_join(vpcsum_pipe_t* pipe);
+int vpcsum_pipe_destroy(vpcsum_pipe_t* pipe);
+
 /* NAT / TTL rewrite + checksum update, in place in the arena; d_rw[i] rewrites packet i.
  * d_status (n bytes): S_DONE, or S_BAD_DESC for a rejected descriptor (nothing written);
  * required with VPCSUM_NAT_STRICT_JAVA. */
@@ -319,6 +337,11 @@ int vpcsum_synth_async(uint8_t* d_arena, uint64_t arena_len, uint32_t n, uint32_
                        uint32_t l3_pad, uint32_t workload, uint64_t seed, uint64_t first_index,
                        vpcsum_desc_t* d_desc, void* stream);
 
+/* Tooling: a grid of `workgroups` x `threads` (a multiple of 64) that stays resident for `micros`
+ * doing nothing but s_sleep -- no memory traffic.  The control of the A/B that asks whether a
+ * resident kernel on another queue, as such, slows launched batches. */
+int vpcsum_spin_probe_async(uint32_t workgroups, uint32_t threads, uint32_t micros, void* stream);
+
 /* Kernel timing on the caller's stream (HIP events). */
 int vpcsum_event_create(void** ev);
 int vpcsum_event_destroy(void* ev);
@@ -350,9 +373,10 @@ int vpcsum_ctx_wait(vpcsum_ctx_t* ctx, uint64_t ticket);
  * vpcsum_ctx_parse_frames -- are handed to a small persistent grid that polls a pinned mailbox,
  * instead of a kernel launch + event wait per batch (the Iface.completeTx flush of a few dozen
  * frames, XDPIface.java:227-243, and the RX poll).  Batches then run one at a time.  The grid leaves
- * after idle_us without a batch and is restarted by the next one; a larger zero-copy batch, which is
- * launched, first stops a grid that has had no batch for 1 ms.  idle_us = 0 stops it (the
- * default).  Staged submits are unaffected. */
+ * after idle_us without a batch and is restarted by the next one; an idle grid costs launched batches
+ * beside it nothing measurable (its pollers use relaxed loads), so larger batches,
+ * which are launched, leave it resident.  idle_us = 0 stops it (the default).  Staged submits are
+ * unaffected. */
 int vpcsum_ctx_set_service(vpcsum_ctx_t* ctx, uint32_t idle_us);
 /* Counters of a context: batches the service ran, service grids launched (either may be NULL). */
 int vpcsum_ctx_stats(vpcsum_ctx_t* ctx, uint64_t* service_batches, uint64_t* service_launches);

@@ -261,6 +261,9 @@ struct Service {
     bool par_valid = false;
     uint32_t posted = 0;                 // last batch published (seq)
     uint64_t idle_ticks = 0;             // 100 MHz ticks
+    uint32_t grid = vpcsum::kServiceGrid;   // workgroups (VPCSUM_SVC_GRID: A/B tooling)
+    uint32_t poll = 1;                      // relay poll mode: relaxed loads (VPCSUM_SVC_POLL: A/B tooling)
+    bool quiesce = false;                   // stop an idle grid before launched batches (VPCSUM_SVC_QUIESCE)
     bool on = false;
     std::chrono::steady_clock::time_point last_post;   // the last batch posted (svc_quiesce)
     bool inline_desc = true;             // descriptors of <= kSvcInlineDesc frames ride in the command line
@@ -337,6 +340,96 @@ int vpcsum_compute_async(const uint8_t* d_arena, uint64_t arena_len, const vpcsu
 
 // NAT on device memory: the rewrite kernel, then (strict Java) the full recompute of the sums it
 // dirtied, written in place -- Java's getRawPacket(0) after the setters.
+}  // extern "C"
+
+// Two batches in flight on the device API (vpcsum.h vpcsum_pipe_*): launches alternate between two
+// streams of the pipe's own, forked from the caller's stream at vpcsum_pipe_begin and joined back
+// into it at vpcsum_pipe_join, so that one launch's ramp-up and drain overlap its neighbour's.
+struct vpcsum_pipe {
+    int device = 0;
+    hipStream_t caller = nullptr;
+    hipStream_t s[2] = {nullptr, nullptr};
+    hipEvent_t fork = nullptr;
+    hipEvent_t done[2] = {nullptr, nullptr};
+    uint32_t next = 0;
+};
+
+static void pipe_free(vpcsum_pipe* p) {
+    for (int i = 0; i < 2; ++i) {
+        if (p->s[i]) {
+            (void)hipStreamSynchronize(p->s[i]);
+            (void)hipStreamDestroy(p->s[i]);
+        }
+        if (p->done[i]) (void)hipEventDestroy(p->done[i]);
+    }
+    if (p->fork) (void)hipEventDestroy(p->fork);
+    delete p;
+}
+
+extern "C" {
+
+int vpcsum_pipe_create(void* stream, vpcsum_pipe_t** out) {
+    try {
+        if (!out) return fail("vpcsum_pipe_create: out is NULL");
+        vpcsum_pipe* p = new vpcsum_pipe();
+        p->caller = (hipStream_t)stream;
+        hipError_t e = hipGetDevice(&p->device);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->s[0], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&p->s[1], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&p->fork, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&p->done[0], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&p->done[1], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            pipe_free(p);
+            return hipfail(e, "vpcsum_pipe_create");
+        }
+        *out = p;
+        return 0;
+    } VPC_CATCH("vpcsum_pipe_create")
+}
+
+int vpcsum_pipe_begin(vpcsum_pipe_t* p) {
+    try {
+        if (!p) return fail("vpcsum_pipe_begin: NULL pipe");
+        VPC_ON_DEVICE(p->device);
+        VPC_CHECK(hipEventRecord(p->fork, p->caller), "vpcsum_pipe_begin: hipEventRecord");
+        for (int i = 0; i < 2; ++i) VPC_CHECK(hipStreamWaitEvent(p->s[i], p->fork, 0), "vpcsum_pipe_begin: hipStreamWaitEvent");
+        return 0;
+    } VPC_CATCH("vpcsum_pipe_begin")
+}
+
+int vpcsum_pipe_compute_async(vpcsum_pipe_t* p, const uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc,
+                              uint32_t n, uint32_t* d_out, uint8_t* d_status, uint32_t mode) {
+    try {
+        if (!p) return fail("vpcsum_pipe_compute_async: NULL pipe");
+        VPC_ON_DEVICE(p->device);
+        const int rc = vpcsum_compute_async(d_arena, arena_len, d_desc, n, d_out, d_status, mode, p->s[p->next & 1]);
+        if (rc == 0) ++p->next;
+        return rc;
+    } VPC_CATCH("vpcsum_pipe_compute_async")
+}
+
+int vpcsum_pipe_join(vpcsum_pipe_t* p) {
+    try {
+        if (!p) return fail("vpcsum_pipe_join: NULL pipe");
+        VPC_ON_DEVICE(p->device);
+        for (int i = 0; i < 2; ++i) {
+            VPC_CHECK(hipEventRecord(p->done[i], p->s[i]), "vpcsum_pipe_join: hipEventRecord");
+            VPC_CHECK(hipStreamWaitEvent(p->caller, p->done[i], 0), "vpcsum_pipe_join: hipStreamWaitEvent");
+        }
+        return 0;
+    } VPC_CATCH("vpcsum_pipe_join")
+}
+
+int vpcsum_pipe_destroy(vpcsum_pipe_t* p) {
+    try {
+        if (!p) return 0;
+        DeviceScope on_dev(p->device);
+        pipe_free(p);
+        return 0;
+    } VPC_CATCH("vpcsum_pipe_destroy")
+}
+
 static int nat_run(uint8_t* d_arena, uint64_t arena_len, const vpcsum_desc_t* d_desc, const void* d_rw, int fmt,
                    uint32_t n, uint8_t* d_status, uint32_t nat_mode, hipStream_t s) {
     if (nat_mode & VPCSUM_NAT_STRICT_JAVA) {
@@ -510,6 +603,15 @@ int vpcsum_synth_async(uint8_t* d_arena, uint64_t arena_len, uint32_t n, uint32_
     } VPC_CATCH("vpcsum_synth_async")
 }
 
+int vpcsum_spin_probe_async(uint32_t workgroups, uint32_t threads, uint32_t micros, void* stream) {
+    try {
+        if (workgroups == 0 || workgroups > 65535 || threads == 0 || threads > 1024 || (threads & 63))
+            return fail("vpcsum_spin_probe_async: bad shape %u x %u", workgroups, threads);
+        VPC_CHECK(launch_spin_probe(workgroups, threads, (uint64_t)micros * 100u, (hipStream_t)stream), "spin probe launch");
+        return 0;
+    } VPC_CATCH("vpcsum_spin_probe_async")
+}
+
 int vpcsum_event_create(void** ev) {
     try {
         if (!ev) return fail("vpcsum_event_create: NULL");
@@ -620,6 +722,12 @@ int vpcsum_ctx_set_service(vpcsum_ctx_t* c, uint32_t idle_us) {
         v.mb->status = (uint64_t)(uintptr_t)v.dh_status;
         v.mb->pre = (uint64_t)(uintptr_t)v.dh_pre;
         v.idle_ticks = (uint64_t)idle_us * 100u;   // s_memrealtime runs at 100 MHz
+        const char* gs = getenv("VPCSUM_SVC_GRID");   // A/B tooling: the grid's workgroups (1..256)
+        if (gs && atoi(gs) >= 1 && atoi(gs) <= 256) v.grid = (uint32_t)atoi(gs);
+        const char* pm = getenv("VPCSUM_SVC_POLL");   // 0: round 5's acquire loads
+        if (pm) v.poll = (uint32_t)atoi(pm) & 7u;
+        const char* q = getenv("VPCSUM_SVC_QUIESCE");
+        v.quiesce = q && q[0] == '1';
         const char* inl = getenv("VPCSUM_SVC_INLINE");
         v.inline_desc = !(inl && inl[0] == '0');
         const char* clamp = getenv("VPCSUM_SVC_CLAMP");   // A/B tooling: 1 = clamped frame loads
@@ -777,7 +885,7 @@ static uint32_t svc_done(const Service& v) { return __atomic_load_n(&v.mb->done,
 static int svc_launch(vpcsum_ctx* c, uint32_t seen) {
     Service& v = c->svc;
     VPC_CHECK(hipMemsetAsync(v.ctr, 0, 16, v.stream), "service counter / relay reset");
-    VPC_CHECK(launch_service(v.dmb, v.ctr, seen, v.idle_ticks, v.stream), "service launch");
+    VPC_CHECK(launch_service(v.dmb, v.ctr, seen, v.idle_ticks, v.stream, v.grid, v.poll), "service launch");
     ++c->svc_launches;
     return 0;
 }
@@ -925,16 +1033,19 @@ static int svc_drain(vpcsum_ctx* c) {
 }
 
 // Before a launched zero-copy batch (more than kSvcBatchMax frames, or a form the grid does not
-// take): a resident service grid that has had no batch for kSvcKeep is stopped first -- it leaves
-// after its current poll -- and the next small batch relaunches it (svc_post).  With an idle grid
-// resident, launched zero-copy batches ran 6-50% slower (tools/flush_latency.cpp: 1,024 parsed
-// frames 36.6 vs 24.5 us); a small batch right after a stop pays a grid launch (32 frames 29 us
-// instead of 13.5), hence the grace period: traffic that alternates small and large batches keeps
-// its grid, a phase of large batches runs without one.
+// take), round 5 stopped a resident grid that had had no batch for kSvcKeep: with an idle grid
+// resident, launched batches ran 6-50% slower.  The cause (round 6, tools/svc_interference.cpp,
+// profiles/r06e_svc_interference.json, r06f_svc_poll.json) was the grid's relay pollers: 31
+// workgroups re-reading the relay word with an agent-scope ACQUIRE load, each one a cache
+// invalidate, while a sleeping grid of the same shape cost nothing.  With relaxed relay loads (the
+// acquire fence after the poll orders the batch, kernels.hip k_csum_service) a resident grid costs
+// the launched batches nothing measurable, so it stays: the stop is now opt-in
+// (VPCSUM_SVC_QUIESCE=1, the A/B of round 5's policy) and a small flush after a large one no
+// longer pays a grid launch.
 constexpr auto kSvcKeep = std::chrono::microseconds(1000);
 static int svc_quiesce(vpcsum_ctx* c) {
     Service& v = c->svc;
-    if (!v.on || hipStreamQuery(v.stream) == hipSuccess) return 0;   // off, or no grid resident
+    if (!v.quiesce || !v.on || hipStreamQuery(v.stream) == hipSuccess) return 0;   // off, or no grid resident
     if (std::chrono::steady_clock::now() - v.last_post < kSvcKeep) return 0;
     if (svc_drain(c) != 0) return -1;
     __atomic_store_n(&v.mb->cmd, kSvcStop | v.posted, __ATOMIC_RELEASE);

@@ -62,8 +62,12 @@ struct SvcFrameRec {
 static_assert(sizeof(SvcFrameRec) == sizeof(vpcsum_desc_t), "a frame record takes a descriptor's slot");
 constexpr uint32_t kSvcMaxPkts = (1u << 23) - 1;   // the command's n field (bits 32..54)
 constexpr uint32_t kSvcBatchMax = 512;              // largest batch the host hands to the service (api.cpp)
-constexpr int kServiceGrid = 32;   // workgroups: 4 waves each, one packet per wave and round
-hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream);
+constexpr int kServiceGrid = 32;   // workgroups: 4 waves each, one packet per wave and round (default)
+hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream,
+                          uint32_t grid = kServiceGrid, uint32_t poll = 0);
+// Tooling: a resident grid of `wgs` workgroups x `threads` that only sleeps (s_sleep) for `ticks`
+// (100 MHz) -- no memory traffic: the control for "a resident kernel on another queue" A/Bs.
+hipError_t launch_spin_probe(uint32_t wgs, uint32_t threads, uint64_t ticks, hipStream_t stream);
 
 // NAT / TTL rewrites (nat.hip).  fmt 0: rw is vpcsum_nat4_t[n], fmt 1: vpcsum_nat_t[n].  With
 // VPCSUM_NAT_STRICT_JAVA the kernel only rewrites and stores Java's dirty flags in flags_out.

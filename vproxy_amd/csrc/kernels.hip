@@ -1385,7 +1385,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_pe
 // (idempotent: checksum fields are excluded from the sums they hold).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* __restrict__ ctr, uint32_t seen,
-                                                      uint64_t idle_ticks) {
+                                                      uint64_t idle_ticks, uint32_t poll) {
     // batch parameters, read over PCIe by thread 0 when the host flags them as changed and kept
     // in LDS across batches: arena, arena_len, arena_w, desc, out, status, opts, pre
     __shared__ uint64_t s_par[8];
@@ -1437,13 +1437,27 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
                 }
             }
         } else if (threadIdx.x == 0) {
-            for (;;) {   // the relay in device memory
-                const uint64_t w = __hip_atomic_load(relay, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            // the relay in device memory, read with RELAXED loads (poll bit 0, the default): the
+            // system-scope acquire after the loop orders the batch's reads.  An acquire load per
+            // poll is a cache invalidate per poll; from 31 workgroups polling it slowed launched
+            // batches beside an idle grid by 6-17% (profiles/r06f_svc_poll.json; relaxed: +0.2%).
+            // A/B tooling (VPCSUM_SVC_POLL): bit 0 clear = acquire loads (round 5), bit 1 back off to
+            // s_sleep 40 after 50 us without a batch, bit 2 read the clock every 64th poll only
+            for (uint32_t k = 0;; ++k) {
+                const uint64_t w = (poll & 1) ? __hip_atomic_load(relay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                              : __hip_atomic_load(relay, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                 if (w & kSvcStop) break;
                 if (w && (uint32_t)w != seen) { got = w; break; }
                 // workgroup 0 relays a stop before it leaves; this bound only guards the grid
                 // against a relay that never comes
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 2 * idle_ticks + 100000) break;
+                if (!(poll & 4) || (k & 63) == 0) {
+                    const uint64_t idle = __builtin_amdgcn_s_memrealtime() - t0;
+                    if (idle > 2 * idle_ticks + 100000) break;
+                    if ((poll & 2) && idle > 5000) {
+                        __builtin_amdgcn_s_sleep(40);
+                        continue;
+                    }
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -1582,8 +1596,19 @@ __global__ __launch_bounds__(256) void k_csum_service(SvcMailbox* mb, uint32_t* 
     }
 }
 
-hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream) {
-    hipLaunchKernelGGL(k_csum_service, dim3(kServiceGrid), dim3(256), 0, stream, d_mb, d_ctr, seen, idle_ticks);
+hipError_t launch_service(SvcMailbox* d_mb, uint32_t* d_ctr, uint32_t seen, uint64_t idle_ticks, hipStream_t stream,
+                          uint32_t grid, uint32_t poll) {
+    hipLaunchKernelGGL(k_csum_service, dim3(grid), dim3(256), 0, stream, d_mb, d_ctr, seen, idle_ticks, poll);
+    return hipGetLastError();
+}
+
+__global__ void k_spin_probe(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(40);
+}
+
+hipError_t launch_spin_probe(uint32_t wgs, uint32_t threads, uint64_t ticks, hipStream_t stream) {
+    hipLaunchKernelGGL(k_spin_probe, dim3(wgs), dim3(threads), 0, stream, ticks);
     return hipGetLastError();
 }
 

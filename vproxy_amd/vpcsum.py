@@ -64,6 +64,8 @@ EXPORTS = [
     "Java_io_vproxy_vpcsum_VPCsum_close", "Java_io_vproxy_vpcsum_VPCsum_setService",
     "Java_io_vproxy_vpcsum_VPCsum_verifyFrames", "Java_io_vproxy_vpcsum_VPCsum_parseFrames",
     "vpcsum_ctx_verify_frames_hsum", "vpcsum_parse_ether_hsum_async", "Java_io_vproxy_vpcsum_VPCsum_verifyFramesHsum",
+    "vpcsum_spin_probe_async", "vpcsum_pipe_create", "vpcsum_pipe_begin", "vpcsum_pipe_compute_async",
+    "vpcsum_pipe_join", "vpcsum_pipe_destroy",
 ]
 
 
@@ -206,6 +208,12 @@ def _declare(L):
         "vpcsum_ctx_stats": ([P, P, P], I),
         "vpcsum_ctx_verify_frames": ([P, P, U64, P, P, U32, P, P, P], I),
         "vpcsum_ctx_verify_frames_hsum": ([P, P, U64, P, P, U32, P, P, P, P], I),
+        "vpcsum_pipe_create": ([P, P], I),
+        "vpcsum_pipe_begin": ([P], I),
+        "vpcsum_pipe_compute_async": ([P, P, U64, P, U32, P, P, U32], I),
+        "vpcsum_pipe_join": ([P], I),
+        "vpcsum_pipe_destroy": ([P], I),
+        "vpcsum_spin_probe_async": ([U32, U32, U32, P], I),
         "vpcsum_ctx_parse_frames": ([P, P, U64, P, P, U32, P, P, P, P], I),
         "vpcsum_ctx_egress_frames": ([P, P, U64, P, P, P, U32, P, P, P], I),
         "vpcsum_ctx_submit": ([P, P, U64, P, U32, P, P, U32, P], I),
@@ -355,6 +363,42 @@ def synth(arena, n: int, stride: int, l3_pad: int, workload: int, seed: int, fir
     _check(lib().vpcsum_synth_async(_ptr(arena) if arena is not None else None, arena.numel() if arena is not None else 0,
                                     n, stride, l3_pad, workload, seed, first_index, _ptr(desc), _stream(stream)),
            "vpcsum_synth_async")
+
+
+class Pipe:
+    """Two batches in flight on the device API (vpcsum_pipe_*): `begin()` forks the pipe's two
+    streams from `stream`, `compute()` launches alternate between them (consecutive batches may run
+    concurrently: their outputs must not overlap), `join()` makes `stream` wait for all of them."""
+
+    def __init__(self, stream=None):
+        h = ctypes.c_void_p()
+        _check(lib().vpcsum_pipe_create(_stream(stream), ctypes.byref(h)), "vpcsum_pipe_create")
+        self.h = h.value
+
+    def begin(self):
+        _check(lib().vpcsum_pipe_begin(self.h), "vpcsum_pipe_begin")
+
+    def compute(self, arena, desc, n: int | None = None, out=None, status=None, mode: int = MODE_COMPUTE,
+                team_log2: int = 0):
+        if n is None:
+            n = desc.numel() * desc.element_size() // 16
+        m = mode | ((team_log2 & 0x1F) << 8) | (((team_log2 >> 5) & 0x7) << 24)
+        _check(lib().vpcsum_pipe_compute_async(self.h, _ptr(arena), arena.numel(), _ptr(desc), n, _ptr(out),
+                                               _ptr(status), m), "vpcsum_pipe_compute_async")
+
+    def join(self):
+        _check(lib().vpcsum_pipe_join(self.h), "vpcsum_pipe_join")
+
+    def close(self):
+        if self.h:
+            lib().vpcsum_pipe_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Event:
