@@ -69,7 +69,8 @@ extern "C" {
                               * setters after its stored L4 sum was verified on ingress
                               * (VPCSUM_S_L4_OK); its L4 sum is updated by RFC 1624 from the
                               * packet's pre-image (vpcsum_pre_t: the words the setters
-                              * overwrote) instead of summed over the segment, its IPv4 header
+                              * overwrote, or with VPCSUM_PRE_HSUM the ingress header sum
+                              * recorded on receipt) instead of summed over the segment, its IPv4 header
                               * sum recomputed.  Only the header is read.  Handled by
                               * vpcsum_pre_async / vpcsum_ctx_submit_pre; vpcsum_compute_async
                               * reads nothing of such a packet, writes nothing into its frame and
@@ -247,7 +248,8 @@ int vpcsum_nat4r_async(uint8_t* d_arena, uint64_t arena_len, const vpcsum_nat4_r
 
 /* Egress sums of NAT'd packets from their pre-images: every descriptor with VPCSUM_F_PRE gets its
  * L4 sum by RFC 1624 eqn. 3 from the stored field, the old words d_pre[i] records and the words now
- * in the frame (HC' = ~(~HC + sum(~m + m'))), its IPv4 header sum (F_IP) recomputed in full from the
+ * in the frame (HC' = ~(~HC + sum(~m + m'))) -- with VPCSUM_PRE_HSUM, the recorded header sum and the
+ * same header words now (any in-place change of them) --, its IPv4 header sum (F_IP) recomputed in full from the
  * header; a UDP stored 0 (no checksum) is summed in full.  The results equal Java's full recompute
  * (getRawPacket(0) after the setters, AbstractPacket.java:15-22) whenever the stored L4 sum was
  * correct before the rewrite -- what ingress verify's VPCSUM_S_L4_OK proves -- and nothing but the
