@@ -1,7 +1,8 @@
 """A mid tier for C3's 576-B class (tooling): K2's default build against the
-same build with a third tier for fast-class packets of more than 4 and at most 40 chunks --
-variants 86 (4 lanes x 10 loads, one trip, 5 waves per SIMD), 87 (4 x 5, two trips), 88 (8 x 5,
-one trip) -- on C3 and its size classes, C2 and C4, compute and verify, in alternated rounds.
+same build with a third tier for fast-class packets of more than 4 and at most 40 chunks, on C3
+and its size classes, C2 and C4, compute and verify, in alternated rounds.  Variants (C3MID_VARIANTS):
+88 (8 lanes x 5 loads, one trip), 90 (the same in workgroup-sorted units only); round 6's first
+run also had 86 (4 x 10, 5 waves per SIMD), 87 (4 x 5, two trips), 89 (4 x 9), since removed.
 Every variant's results are compared with the default build's first.  Output: one JSON line."""
 import json, os, sys
 import numpy as np, torch
@@ -9,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vproxy_amd import vpcsum as V  # noqa: E402
 from bench import WORKLOADS, algorithmic_bytes  # noqa: E402
 
-VARIANTS = [0, 86, 87, 88]
+VARIANTS = [int(v) for v in os.environ.get("C3MID_VARIANTS", "0,88,90").split(",")]
 ROUNDS = int(os.environ.get("C3MID_ROUNDS", "3"))
 
 
@@ -71,5 +72,6 @@ for name in res:
     base = float(np.median(res[name]["0"]))
     summary[name] = {v: {"GBps": res[name][v], "median_vs_default": round(float(np.median(res[name][v])) / base - 1, 4)}
                      for v in res[name]}
-print(json.dumps({"variants": {"0": "default", "86": "mid tier 4x10 (5 waves/SIMD)", "87": "mid tier 4x5",
-                               "88": "mid tier 8x5"}, "rounds": ROUNDS, "cases": summary}))
+names = {"0": "default", "86": "mid tier 4x10 (5 waves/SIMD)", "87": "mid tier 4x5", "88": "mid tier 8x5",
+         "89": "mid tier 4x9 (5 waves/SIMD)", "90": "mid tier 8x5, workgroup-sorted units only"}
+print(json.dumps({"variants": {str(v): names.get(str(v), "") for v in VARIANTS}, "rounds": ROUNDS, "cases": summary}))
