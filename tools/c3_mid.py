@@ -2,7 +2,9 @@
 same build with a third tier for fast-class packets of more than 4 and at most 40 chunks, on C3
 and its size classes, C2 and C4, compute and verify, in alternated rounds.  Variants (C3MID_VARIANTS):
 88 (8 lanes x 5 loads, one trip), 90 (the same in workgroup-sorted units only); round 6's first
-run also had 86 (4 x 10, 5 waves per SIMD), 87 (4 x 5, two trips), 89 (4 x 9), since removed.
+run also had 86 (4 x 10, 5 waves per SIMD), 87 (4 x 5, two trips), 89 (4 x 9).  None was kept
+(DESIGN.md §5 "C3"): the variants live in the library of commit 4fada6b ("C3: mid-tier A/B
+variants"); build that tree's kernels.hip to re-run this.
 Every variant's results are compared with the default build's first.  Output: one JSON line."""
 import json, os, sys
 import numpy as np, torch

@@ -835,11 +835,7 @@ constexpr uint64_t kWinSpan = kWinBytes + 65536;
 // ROT: large-tier rotation of the wave's slot order, by multiplier |ROT| of the wave index;
 // ROT > 0 rotates whole iterations (64 / TEAM packets), ROT < 0 single slots.
 // WGS: workgroup-sorted units on mixed batches (below).
-// TM, UM: a mid tier (with a small tier): fast-class packets of more than TS x US and at most
-// kMidChunks chunks (C3's 576-B class) streamed by teams of |TM| lanes x UM loads; TM < 0: in
-// workgroup-sorted units only (mixed batches), the per-wave units as without it.
-constexpr int kMidChunks = 40;
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false, bool WGS = false, int TM = 0, int UM = 1>
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int IL, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false, bool WGS = false>
 __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                        const uint4* __restrict__ desc, uint32_t n,
                                        uint32_t* __restrict__ out, uint8_t* __restrict__ status,
@@ -945,8 +941,6 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
     // in the builds without WGS (one loop with a runtime mode cost C2 0.9%)
     auto unit_loop = [&](auto wgm_tag) {
     constexpr bool WGM = decltype(wgm_tag)::value;
-    constexpr bool MID = TM > 0 || (TM < 0 && WGM);
-    constexpr int TMa = TM < 0 ? -TM : (TM > 0 ? TM : 1);
     for (uint32_t Pn; (WGM ? P0 - (uint32_t)wid * 64u : P0) < n; P0 = Pn) {
         // ---- phase A: this lane's packet ----
         const uint4 dv = dnext;
@@ -991,7 +985,6 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         int fld = -1;
         int key = 0;
         int n_small = 0, n_cls = 0;   // n_cls: distinct cost classes in the large tier
-        int n_mid = 0;                // TM: slots [n_small, n_mid) are the mid tier's
         bool fastu = false;           // window unit (SF): sums in fsums, no slots
         uint4 fsums = make_uint4(0, 0, 0, 0);
         // Window units (SF): the 64 packets of the unit have one shape (descriptor fields, flags
@@ -1192,7 +1185,6 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
             // then trips of the large tier's team loop, the slow class last
             if (!bad) {
                 if (TS > 0 && fastc && pl.nch <= TS * US) key = 1;
-                else if (TS > 0 && MID && fastc && pl.nch <= kMidChunks) key = 2;
                 else key = fastc ? 2 + min((pl.nch + TEAM * U - 1) / (TEAM * U), 12) : 15;
             }
             uint32_t rank = 0, cnt = 0;
@@ -1206,9 +1198,8 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                     kp = cnt;
                 }
                 cnt += (uint32_t)__popcll(m);
-                if (b >= (MID ? 3 : 2) && m) ++n_cls;
+                if (b >= 2 && m) ++n_cls;
                 if (b == 1) n_small = (int)cnt;   // keys 0 and 1 go to the small tier
-                if (MID && b <= 2) n_mid = (int)cnt;   // also when the loop ends before class 2
             }
             uint32_t si = (uint32_t)wid * 64u + rank;   // this packet's slot among the workgroup's 256
             if (WGM) {
@@ -1226,7 +1217,6 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
                 const uint32_t first = incl - tot + before - kp;   // class b's first slot, minus its offset here
                 si = (uint32_t)__builtin_amdgcn_ds_bpermute(key << 2, (int)first) + rank;
                 n_small = __builtin_amdgcn_readlane((int)(incl - tot), 2);
-                if (MID) n_mid = __builtin_amdgcn_readlane((int)(incl - tot), 3);
             }
             key = (int)si;   // from here on: this packet's slot
             {
@@ -1308,15 +1298,8 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
         const int it0 = WGM ? wid : 0, istep = WGM ? 4 : 1;
         if (TS > 0) {
             stream_tier<(TS > 0 ? TS : 1), US, VERIFY, NT>(rsrc, tslots, lane, 0, n_small, 0u, it0, istep);
-            // WGM: each tier starts with the wave after the one that took the previous tier's last iteration
-            int it0l = WGM ? (it0 + 4 - (((n_small + 64 / (TS > 0 ? TS : 1) - 1) / (64 / (TS > 0 ? TS : 1))) & 3)) & 3 : 0;
-            int l_begin = n_small;
-            if (MID) {
-                stream_tier<TMa, UM, VERIFY, NT>(rsrc, tslots, lane, n_small, n_mid, 0u, it0l, istep);
-                if (WGM) it0l = (it0l + 4 - (((n_mid - n_small + 64 / TMa - 1) / (64 / TMa)) & 3)) & 3;
-                l_begin = n_mid;
-            }
-            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0), WT>(rsrc, tslots, lane, l_begin, t_end,
+            const int it0l = WGM ? (it0 + 4 - (((n_small + 64 / (TS > 0 ? TS : 1) - 1) / (64 / (TS > 0 ? TS : 1))) & 3)) & 3 : 0;
+            stream_tier<TEAM, U, VERIFY, NT, (ROT < 0), WT>(rsrc, tslots, lane, n_small, t_end,
                                              // rotated only when the tier is one cost class: in a
                                              // sorted mixed tier the wrap would pair unlike sizes
                                              (ROT && n_cls == 1 && !WGM) ? (blk * 4u + (uint32_t)wid) * (uint32_t)(ROT < 0 ? -ROT : ROT) : 0u,
@@ -1368,7 +1351,7 @@ __device__ __forceinline__ void k2_run(const uint8_t* __restrict__ arena, uint64
 // count: left alone, the compiler gave them 95 and 92 (5 waves) -- the verify build for its stored
 // fields, the staging build because its 26 KB of LDS let it budget for fewer resident waves
 // (DESIGN.md §5 items 25, 28).  tests/test_kernel_resources.py holds all of them to 80, no scratch.
-template <int TEAM, int U, int TS, int US, bool VERIFY, int WPE, int IL, int ROT, bool SF, bool WT, bool DS, bool WIN = false, bool WGS = false, int TM = 0, int UM = 1>
+template <int TEAM, int U, int TS, int US, bool VERIFY, int WPE, int IL, int ROT, bool SF, bool WT, bool DS, bool WIN = false, bool WGS = false>
 constexpr int k2_waves_per_eu() {
     return WPE > 1 ? WPE
                    : (TEAM == kDefaultTeam && U == kDefaultUnroll && TS == kSmallTeam && US == kSmallUnroll &&
@@ -1377,13 +1360,13 @@ constexpr int k2_waves_per_eu() {
                          : 1;
 }
 
-template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false, bool WGS = false, int TM = 0, int UM = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_per_eu<TEAM, U, TS, US, VERIFY, WPE, IL, ROT, SF, WT, DS, WIN, WGS, TM, UM>()))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
+template <int TEAM, int U, int TS, int US, bool VERIFY, bool NT, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false, bool WGS = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(k2_waves_per_eu<TEAM, U, TS, US, VERIFY, WPE, IL, ROT, SF, WT, DS, WIN, WGS>()))) void k_csum_d(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                 const uint4* __restrict__ desc, uint32_t n,
                                                 uint32_t* __restrict__ out, uint8_t* __restrict__ status,
                                                 const uint8_t* __restrict__ flags_override,
                                                 uint8_t* __restrict__ arena_w, uint32_t low_grid) {
-    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS, WIN, WGS, TM, UM>(arena, arena_len, desc, n, out, status, flags_override,
+    k2_run<TEAM, U, TS, US, VERIFY, NT, IL, ROT, SF, WT, DS, WIN, WGS>(arena, arena_len, desc, n, out, status, flags_override,
                                                                        arena_w, low_grid, blockIdx.x, gridDim.x);
 }
 
@@ -1652,7 +1635,7 @@ static uint32_t default_low_grid() {
     return (uint32_t)num_cus(dev) * 2u;
 }
 
-template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false, bool WGS = false, int TM = 0, int UM = 1>
+template <int TEAM, int U, int TS = 0, int US = 1, int WPE = 1, int IL = 0, int ROT = 0, bool SF = false, bool WT = false, bool DS = false, bool WIN = false, bool WGS = false>
 static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsum_desc_t* desc, uint32_t n,
                            uint32_t* out, uint8_t* status, const uint8_t* flags_override, bool verify, bool nt,
                            uint8_t* arena_w, int grid, bool adapt, hipStream_t stream) {
@@ -1675,7 +1658,7 @@ static hipError_t launch_d(const uint8_t* arena, uint64_t arena_len, const vpcsu
     const uint32_t cus = (uint32_t)num_cus(dev);
 #define VPC_LAUNCH(V, N)                                                                                         \
     do {                                                                                                         \
-        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT, DS, WIN, WGS, TM, UM>;                             \
+        auto kern = k_csum_d<TEAM, U, TS, US, V, N, WPE, IL, ROT, SF, WT, DS, WIN, WGS>;                             \
         uint32_t gg = g;                                                                                         \
         if (dense) {                                                                                             \
             static const uint32_t res = resident_wgs((const void*)kern);                                         \
@@ -1749,15 +1732,6 @@ hipError_t launch_csum(const uint8_t* arena, uint64_t arena_len, const vpcsum_de
         case 84:
             if (arena_len > kMaxBufArena) return hipErrorInvalidValue;
             return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true, false, true>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
-        // 88 / 90: 84 with a mid tier of 8 lanes x 5 loads for C3's 576-B class (A/B): in every
-        // unit / in workgroup-sorted units only.  Teams of 4 lanes x 9 or 10 loads (one trip) and
-        // 4 x 5 (two trips) lost 9-15% on that class (profiles/r06i_c3_mid_tier.json)
-        case 88:
-        case 90:
-            if (arena_len > kMaxBufArena) return hipErrorInvalidValue;
-            if (team_log2 == 88)
-                return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true, false, true, 8, 5>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
-            return launch_d<kDefaultTeam, kDefaultUnroll, kSmallTeam, kSmallUnroll, 1, 0, kDefaultRot, true, false, true, false, true, -8, 5>(arena, arena_len, desc, n, out, status, flags_override, verify, nt, arena_w, grid, adapt, stream);
         case 70:
         case 0:
             // Arenas past 4 GiB: K2 with a pass per 2-GiB window its units' packets start in (see
