@@ -30,8 +30,7 @@ torch.cuda.synchronize()
 # vpcsum_ctx_register_arena, as a umem would be): the pipeline's MODE_WRITE stores through it
 arena_np = d_arena.cpu().numpy().copy()
 h_arena = torch.from_numpy(arena_np).pin_memory()   # hipHostMalloc'd copy for the zero-copy kernel
-h_desc_t = d_desc.cpu().pin_memory()
-desc = h_desc_t.numpy().view(V.DESC_DTYPE)
+desc = d_desc.cpu().numpy().view(V.DESC_DTYPE).copy()
 nbytes = algorithmic_bytes(desc)
 ref = torch.zeros(n, dtype=torch.int32, device="cuda")
 V.compute(d_arena, d_desc, n, ref, None)
@@ -41,8 +40,11 @@ del d_arena
 
 ctx = V.Context(0, max_arena=(n // 4) * stride + 4096, max_pkts=n // 4)
 ctx.register(arena_np)
-out = torch.zeros(n, dtype=torch.int32).pin_memory().numpy().view(np.uint32)
-# torch pin_memory() buffers are hipHostMalloc'd: the context recognises them as page-locked
+out = np.zeros(n, np.uint32)
+# the pipeline's descriptors and results are page-locked by the context too (round 6: a context
+# copies asynchronously only from memory it locked itself)
+ctx.register(desc)
+ctx.register(out)
 
 pipe = {}
 for chunks in (4, 8, 16, 32):
@@ -83,7 +85,7 @@ res["pipeline_h2d_kernel_d2h_write_frames"] = pipe
 
 # zero-copy: kernel reads the page-locked host arena in place (PCIe reads, no staging copy)
 zc_out = torch.zeros(n, dtype=torch.int32, device="cuda")
-h_desc_dev = h_desc_t.cuda()
+h_desc_dev = d_desc
 V.compute(h_arena, h_desc_dev, n, zc_out, None)
 torch.cuda.synchronize()
 t = time.perf_counter()
