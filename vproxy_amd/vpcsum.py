@@ -142,8 +142,19 @@ def _reg_drop(ptr: int):
         if not lst:
             del _live_regs[ptr]
         covered = any(q <= ptr < q + max(m) for q, m in _live_regs.items())
-    if _AUDIT and not covered and (hip_holds_registered(ptr) or hip_holds_registered(ptr + n - 1)):
+    if _AUDIT and not covered and any(hip_holds_registered(q) for q in _audit_points(ptr, n)):
         _stale.append((ptr, n))
+
+
+def _audit_points(ptr: int, n: int, cap: int = 256) -> list[int]:
+    """Addresses of a released range HIP is asked about: both ends and one address in every page
+    between them (at most `cap`, evenly spread over a larger range)."""
+    first, last = ptr, ptr + n - 1
+    pages = (last >> 12) - (ptr >> 12) + 1
+    step = max(1, -(-pages // cap))
+    pts = [first, last]
+    pts += [((ptr >> 12) + k) << 12 for k in range(1, pages - 1, step)]
+    return pts
 
 
 def released_ranges(clear: bool = True) -> list[tuple[int, int]]:
