@@ -146,3 +146,17 @@ def test_default_group_calls_race_shutdown_without_gpu(libpath):
     for t in ts:
         t.join()
     assert not bad
+
+
+def test_registration_audit_covers_every_page():
+    """The release audit (vpcsum._audit_points) asks HIP about both ends of a released range and
+    one address in every page between them, at most 256 spread evenly over a larger range."""
+    from vproxy_amd.vpcsum import _audit_points
+    p, n = 0x1010, 164238
+    pts = _audit_points(p, n)
+    assert p in pts and p + n - 1 in pts
+    assert {q >> 12 for q in pts} == set(range(p >> 12, ((p + n - 1) >> 12) + 1))
+    assert all(p <= q < p + n for q in pts)
+    big = _audit_points(0x10, 1 << 30)
+    assert len(big) <= 258 and min(big) == 0x10 and max(big) == 0x10 + (1 << 30) - 1
+    assert _audit_points(0x2000, 1) == [0x2000, 0x2000]
