@@ -10,6 +10,9 @@ rounds alternated (Gpps over the 10M packets, HIP events):
   halves2s   the two halves on two streams forked from one and joined back (concurrent)
   quarters4s four quarters on four streams
   half       the first 5M packets alone (a half-size launch; rate over its own packets)
+  allocs     the same 10M packets as two separate 10.24-GB allocations (5M each, as the two ranks
+             hold them), one launch each, one after the other
+  allocs2s   the two allocations' launches on two streams at once
 Output: one JSON line."""
 import json
 import os
@@ -32,6 +35,14 @@ g = np.random.default_rng(SEED)
 rw_np.view(np.uint8).reshape(-1, 16)[:, :12] = g.integers(0, 256, (n, 12), dtype=np.uint8)
 rw_np["mask"] = V.NAT_SRC | V.NAT_DST | V.NAT_SPORT | V.NAT_DPORT
 rw = torch.from_numpy(rw_np.view(np.uint8).copy()).cuda()
+h = n // 2
+sep = []   # the two ranks' layout: each half its own allocation, frames synthesized in place
+for k in range(2):
+    a2 = torch.zeros(h * stride, dtype=torch.uint8, device="cuda")
+    d2 = torch.zeros(h * 16, dtype=torch.uint8, device="cuda")
+    V.synth(a2, h, stride, 0, sid, SEED, k * h, d2)
+    V.compute(a2, d2, h, None, None, V.MODE_WRITE)
+    sep.append((a2, d2, rw[k * h * 16:(k + 1) * h * 16]))
 torch.cuda.synchronize()
 main = torch.cuda.current_stream()
 side = [torch.cuda.Stream() for _ in range(4)]
@@ -48,6 +59,19 @@ def run(form):
     elif form == "half":
         dd, rr, m = part(0, 2)
         V.nat4(arena, dd, rr, m, None, V.NAT_RFC1624, stream=main)
+    elif form == "allocs":
+        for a2, d2, r2 in sep:
+            V.nat4(a2, d2, r2, h, None, V.NAT_RFC1624, stream=main)
+    elif form == "allocs2s":
+        e = torch.cuda.Event()
+        e.record(main)
+        for k, (a2, d2, r2) in enumerate(sep):
+            side[k].wait_event(e)
+            V.nat4(a2, d2, r2, h, None, V.NAT_RFC1624, stream=side[k])
+        for k in range(2):
+            ev = torch.cuda.Event()
+            ev.record(side[k])
+            main.wait_event(ev)
     elif form == "halves":
         for k in range(2):
             dd, rr, m = part(k, 2)
@@ -66,7 +90,7 @@ def run(form):
             main.wait_event(ev)
 
 
-FORMS = ["one", "halves", "halves2s", "quarters4s", "half"]
+FORMS = ["one", "halves", "halves2s", "quarters4s", "half", "allocs", "allocs2s"]
 res = {f: [] for f in FORMS}
 for _ in range(300):   # clocks up
     run("one")
